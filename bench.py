@@ -1,0 +1,215 @@
+"""Benchmark of the MI355X-native SGM hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config c3|c2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on): 1920x1080 stereo
+pairs, D = 256, 9x7 census + Hamming cost, 8-path SGM, WTA + uniqueness + subpixel +
+LR check (`--config c2`: D = 128, no subpixel / LR). A step = one pass of the hot path over
+F synthetic frames per rank, inputs resident in HBM before timing. Frames are independent,
+so each rank owns its own frames (frame shard, weak scaling, no data-path collective); the
+only collectives are the timing barrier and the max-over-ranks reduction.
+
+`roofline` is the dominant kernel (algorithmic bytes / its average HIP-event duration over
+the timed region); `pipeline` is the whole frame (SURVEY §8d B_alg / per-frame device
+time). `cpu_baseline` times the CPU port (oracle) on a bounded sample on rank 0 at N = 1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
+METRIC = "stereo pairs/sec + ms/frame, 1920×1080 D=256 8-path SGM, 1/2/4/8 MI355X"
+
+CONFIGS = {
+    "c3": dict(name="C3: 1920x1080 D=256 census9x7 8-path SGM + subpixel + LR-check", w=1920, h=1080, D=256,
+               subpixel=1, lr_check=1),
+    "c2": dict(name="C2: 1920x1080 D=128 census9x7 8-path SGM (no subpixel / LR)", w=1920, h=1080, D=128,
+               subpixel=0, lr_check=0),
+}
+
+
+def shard_frames(n_frames_per_rank, rank, seed0=0):
+    """Frame ids owned by `rank` (distinct synthetic frames per rank)."""
+    return [seed0 + rank * n_frames_per_rank + i for i in range(n_frames_per_rank)]
+
+
+def algorithmic_bytes(w, h, D, width1):
+    """SURVEY §8d B_alg per stereo pair, evaluated on the aggregated cells (width1 x H x D):
+    2 B/px images in + 8 u8 path volumes written + read once (16 B/cell) + 2 B/px out."""
+    return 4.0 * w * h + 16.0 * width1 * h * D
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch from the committed PMC profile (profiles/*_pmc.json), if any."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg, budget_s=20.0):
+    """Times the CPU port of the same workload (oracle, multi-threaded C) on host cores."""
+    import numpy as np
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sgm_oracle", os.path.join(ROOT, "oracle", "sgm_oracle.py"))
+    orc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(orc)
+    import __graft_entry__ as ge
+    synth = ge._load_file("sgm_synth", os.path.join(ge.PKG_DIR, "synth.py"))
+    left, right, _ = synth.stereo_pair(cfg["h"], cfg["w"], 0, cfg["D"], seed=12345, with_truth=False)
+    p = orc.make_params(orc.MODE_CENSUS8, num_disparities=cfg["D"], subpixel=cfg["subpixel"],
+                        lr_check=cfg["lr_check"])
+    threads = orc.num_threads()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        orc.match(p, left, right)
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 2 or n >= 8:
+            break
+    dt = time.perf_counter() - t0
+    out = {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+           "sample": f"{n} full {cfg['w']}x{cfg['h']} D={cfg['D']} frames of the same census-SGM workload, "
+                     f"oracle/sgm_oracle.c (OpenMP over lines, {threads} threads)"}
+    # the reference's own CPU path: OpenCV-SGBM restatement, single thread, same geometry
+    pr = orc.make_params(orc.MODE_OCV_SGBM5, min_disparity=0, num_disparities=cfg["D"], block_size=5,
+                         speckle_window_size=0)
+    orc.set_threads(1)
+    t0 = time.perf_counter()
+    orc.match(pr, left, right)
+    dt1 = time.perf_counter() - t0
+    orc.set_threads(threads)
+    out["reference_path"] = {"value": 1.0 / dt1, "unit": "pairs/s", "cores": 1, "kind": "port",
+                             "sample": f"1 frame {cfg['w']}x{cfg['h']} D={cfg['D']} OpenCV-StereoSGBM "
+                                       f"MODE_SGBM restatement (block 5), single-threaded like OpenCV"}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=8, help="frames per rank per step")
+    ap.add_argument("--distinct", type=int, default=4, help="distinct synthetic pairs per rank")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    device = torch.cuda.current_device()
+
+    pkg = ge.load_package()
+    synth = ge._load_file("sgm_synth", os.path.join(ge.PKG_DIR, "synth.py"))
+    W, H, D = cfg["w"], cfg["h"], cfg["D"]
+    params = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=0, p1=10, p2=120,
+                                uniqueness_ratio=5, subpixel=cfg["subpixel"], lr_check=cfg["lr_check"],
+                                disp12_max_diff=1, median=0, speckle_window_size=0)
+    eng = pkg.Engine(device, params)
+
+    # inputs resident in HBM before timing (distinct frames per rank)
+    ids = shard_frames(args.distinct, rank)
+    dl, dr = [], []
+    for i in ids:
+        l, r, _ = synth.stereo_pair(H, W, 0, D, seed=i, with_truth=False)
+        dl.append(torch.from_numpy(l).to(device))
+        dr.append(torch.from_numpy(r).to(device))
+    out = torch.empty((args.frames, H, W), dtype=torch.int16, device=device)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        for f in range(args.frames):
+            k = f % len(dl)
+            eng.match_device(dl[k].data_ptr(), dr[k].data_ptr(), W, H, W, out[f].data_ptr(), W, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    eng.set_profiling(True)          # hipEvents around every stage, no host sync per frame
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stages = eng.stage_times()
+    n_prof = eng.profiled_matches()
+    eng.set_profiling(False)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    frames_total = args.frames * args.steps * world
+    value = frames_total / elapsed_max
+    ms_per_step = elapsed_max * 1e3 / args.steps
+
+    if rank == 0:
+        g = pkg.effective_geometry(params, W, H)
+        dev_frame_ms = sum(s[1] for s in stages)
+        dom = max(stages, key=lambda s: s[1])
+        dom_achieved = dom[2] / (dom[1] * 1e-3) / 1e9
+        b_alg = algorithmic_bytes(W, H, D, g["width1"])
+        pipe_achieved = b_alg / (dev_frame_ms * 1e-3) / 1e9
+        pmc = load_pmc_traffic()
+        traffic = None
+        if pmc and pmc.get("config") == args.config:
+            traffic = pmc.get("kernels", {}).get(dom[0], {}).get("hbm_bytes_per_launch")
+        res = {
+            "metric": METRIC, "value": round(value, 3), "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "ms_per_frame": round(elapsed_max * 1e3 / (args.frames * args.steps), 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (numpy PCG64 textured pairs, piecewise-planar truth, resident in HBM)",
+            "config": {"workload": cfg["name"], "width": W, "height": H, "num_disparities": D,
+                       "frames_per_rank_per_step": args.frames, "global_batch": args.frames * world,
+                       "distinct_frames_per_rank": args.distinct, "parallelism": f"frame-shard x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(dom_achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom_achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": dom[2],
+                         "avg_launch_ms": round(dom[1], 5)},
+            "pipeline": {"bound": "hbm", "B_alg_per_pair": b_alg, "device_ms_per_pair": round(dev_frame_ms, 5),
+                         "achieved": round(pipe_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(pipe_achieved / HBM_PEAK_GBS, 4)},
+            "stages": [{"name": n, "avg_ms": round(ms, 5), "alg_bytes": b, "GBps": round(b / (ms * 1e-3) / 1e9, 1)}
+                       for n, ms, b in stages],
+            "profiled_frames": n_prof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(res))
+    eng.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,506 @@
+"""MI355X-native SGM disparity engine — Python host mirror of the reference's plugin surface.
+
+The compute path is libsgm_hip.so (hand-written HIP for gfx950, csrc/) behind the C-ABI in
+include/sgm_hip.h. This module binds it with ctypes and mirrors, name for name, the
+reference's host-side interface for the hot path so tests read like the reference's code:
+
+  * `MatcherHIPSGM`      — AbstractStereoMatcher subclass semantics
+                           (reference include/stereoMatcher/abstractStereoMatcher.h:12-92,
+                            setters as src/stereoMatcher/matcherOpenCVSGBM.cpp:53-110)
+  * `stereo_match`       — generate_disparity.cpp:334-368
+  * `process_disparity`  — generate_disparity.cpp:398-456 (x1/16, depth window, MISSING_Z)
+  * `parameter_callback` — generate_disparity.cpp:735-845 (cfg sanitising, matcher swap)
+
+There is no CPU fallback: if the HIP library is missing or no device is visible, matching
+fails loudly (MatcherHIPSGM.forwardMatch returns -1 exactly like the OpenCV wrapper on an
+exception, and `Engine` raises).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsgm_hip.so")
+
+MODE_OCV_SGBM5 = 0
+MODE_OCV_HH8 = 1
+MODE_CENSUS8 = 2
+
+SGM_OK, SGM_ERR_ARG, SGM_ERR_PARAM, SGM_ERR_DEVICE, SGM_ERR_ALLOC, SGM_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
+
+# reference enum (cfg/i3DR_Disparity.cfg:11-17) + the new entry this engine adds
+CV_StereoBM, CV_StereoSGBM, I3DR_StereoSGM, CV_StereoBMCuda, CV_StereoBPCuda, CV_StereoCSBPCuda = range(6)
+HIP_StereoSGM = 6
+
+MISSING_Z = 10000.0  # image_geometry::StereoCameraModel::MISSING_Z
+
+EXPORTS = [
+    "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
+    "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_batch", "sgm_synchronize", "sgm_last_error",
+    "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
+    "sgm_debug_census",
+    "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
+]
+
+
+class SgmParams(ctypes.Structure):
+    """`sgm_params` of include/sgm_hip.h."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "mode", "min_disparity", "num_disparities", "block_size", "p1", "p2",
+        "uniqueness_ratio", "disp12_max_diff", "prefilter_cap", "speckle_window_size",
+        "speckle_range", "subpixel", "lr_check", "median")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+    def copy(self, **kw):
+        p = SgmParams()
+        for n, _ in self._fields_:
+            setattr(p, n, getattr(self, n))
+        for k, v in kw.items():
+            setattr(p, k, int(v))
+        return p
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libsgm_hip.so; raises if it is missing (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"libsgm_hip.so not found at {path}: run build() / build_ext.py first")
+    L = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.sgm_device_count.restype = ci
+    L.sgm_create.argtypes = [P(ctypes.c_void_p), ci]
+    L.sgm_destroy.argtypes = [vp]
+    L.sgm_destroy.restype = None
+    L.sgm_default_params.argtypes = [P(SgmParams), ci]
+    L.sgm_default_params.restype = None
+    L.sgm_set_params.argtypes = [vp, P(SgmParams)]
+    L.sgm_get_params.argtypes = [vp, P(SgmParams)]
+    L.sgm_check_params.argtypes = [P(SgmParams), ci, ci]
+    L.sgm_match.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz]
+    L.sgm_match_device.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, vp]
+    L.sgm_match_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, P(ci), ci]
+    L.sgm_synchronize.argtypes = [vp]
+    L.sgm_last_error.argtypes = [vp]
+    L.sgm_last_error.restype = ctypes.c_char_p
+    L.sgm_set_profiling.argtypes = [vp, ci]
+    L.sgm_get_stage_times.argtypes = [vp, P(ctypes.c_float), ci]
+    L.sgm_profiled_matches.argtypes = [vp]
+    L.sgm_stage_name.argtypes = [vp, ci]
+    L.sgm_stage_name.restype = ctypes.c_char_p
+    L.sgm_stage_bytes.argtypes = [vp, ci]
+    L.sgm_stage_bytes.restype = ctypes.c_double
+    L.sgm_debug_census.argtypes = [vp, vp, ci, ci, sz, vp]
+    L.sgm_debug_census_path.argtypes = [vp, vp, vp, ci, ci, sz, ci, vp]
+    L.sgm_debug_ocv_cost.argtypes = [vp, vp, vp, ci, ci, sz, vp]
+    L.sgm_debug_median3.argtypes = [vp, vp, ci, ci]
+    L.sgm_debug_speckle.argtypes = [vp, vp, ci, ci, ci, ci, ci]
+    _lib = L
+    return L
+
+
+def default_params(mode=MODE_CENSUS8, **kw):
+    p = SgmParams()
+    load_library().sgm_default_params(ctypes.byref(p), int(mode))
+    for k, v in kw.items():
+        setattr(p, k, int(v))
+    return p
+
+
+def device_count():
+    return int(load_library().sgm_device_count())
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class SGMError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sgm status {code}: {msg}")
+        self.code = code
+
+
+def effective_geometry(params, width, height):
+    """(minX1, maxX1, width1, D, invalid) — OpenCV computeDisparitySGBM column range."""
+    minD, D = params.min_disparity, params.num_disparities
+    maxD = minD + D
+    minX1 = max(maxD, 0)
+    maxX1 = width + min(minD, 0)
+    return dict(minX1=minX1, maxX1=maxX1, width1=maxX1 - minX1, D=D, invalid=(minD - 1) * 16)
+
+
+class Engine:
+    """Owning wrapper of one `sgm_handle` (one device, one stream, one workspace)."""
+
+    def __init__(self, device=0, params=None):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.sgm_create(ctypes.byref(h), int(device))
+        if rc != SGM_OK:
+            raise SGMError(rc, f"cannot open HIP device {device} ({self.lib.sgm_device_count()} visible)")
+        self.h = h
+        self.device = device
+        if params is not None:
+            self.set_params(params)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.sgm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self):
+        e = self.lib.sgm_last_error(self.h)
+        return e.decode() if e else ""
+
+    def _check(self, rc):
+        if rc != SGM_OK:
+            raise SGMError(rc, self.error())
+
+    def set_params(self, p):
+        self._check(self.lib.sgm_set_params(self.h, ctypes.byref(p)))
+
+    def get_params(self):
+        p = SgmParams()
+        self._check(self.lib.sgm_get_params(self.h, ctypes.byref(p)))
+        return p
+
+    def match(self, left, right):
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        if left.shape != right.shape or left.ndim != 2:
+            raise ValueError("left/right must be equal-size 2-D u8 images")
+        h, w = left.shape
+        out = np.empty((h, w), np.int16)
+        self._check(self.lib.sgm_match(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w))
+        return out
+
+    def match_device(self, d_left, d_right, width, height, stride, d_out, out_stride, stream=None):
+        """Device pointers (ints) already resident in HBM; async on `stream` (int handle)."""
+        self._check(self.lib.sgm_match_device(self.h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right), width,
+                                              height, stride, ctypes.c_void_p(d_out), out_stride,
+                                              ctypes.c_void_p(stream) if stream else None))
+
+    def synchronize(self):
+        self._check(self.lib.sgm_synchronize(self.h))
+
+    def match_batch(self, lefts, rights, devices=None):
+        n = len(lefts)
+        lefts = [np.ascontiguousarray(a, np.uint8) for a in lefts]
+        rights = [np.ascontiguousarray(a, np.uint8) for a in rights]
+        h, w = lefts[0].shape
+        outs = [np.empty((h, w), np.int16) for _ in range(n)]
+        arr = ctypes.c_void_p * max(n, 1)
+        L = arr(*[a.ctypes.data for a in lefts])
+        R = arr(*[a.ctypes.data for a in rights])
+        O = arr(*[a.ctypes.data for a in outs])
+        if devices:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            nd = len(devices)
+        else:
+            devs, nd = None, 0
+        self._check(self.lib.sgm_match_batch(self.h, L, R, n, w, h, w, O, w, devs, nd))
+        return outs
+
+    # -- profiling -------------------------------------------------------------------------
+    def set_profiling(self, on=True):
+        self._check(self.lib.sgm_set_profiling(self.h, 1 if on else 0))
+
+    def profiled_matches(self):
+        return int(self.lib.sgm_profiled_matches(self.h))
+
+    def stage_times(self):
+        """[(stage, average ms over the profiled matches, algorithmic bytes per match)]"""
+        buf = (ctypes.c_float * 16)()
+        n = self.lib.sgm_get_stage_times(self.h, buf, 16)
+        if n < 0:
+            raise SGMError(n, self.error())
+        return [(self.lib.sgm_stage_name(self.h, i).decode(), float(buf[i]),
+                 float(self.lib.sgm_stage_bytes(self.h, i))) for i in range(n)]
+
+    # -- stage entry points (parity tests) -------------------------------------------------
+    def census(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        out = np.empty((h, w), np.uint64)
+        self._check(self.lib.sgm_debug_census(self.h, _ptr(img), w, h, w, _ptr(out)))
+        return out
+
+    def census_path(self, left, right, direction):
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        h, w = left.shape
+        e = effective_geometry(self.get_params(), w, h)
+        vol = np.zeros((h, max(e["width1"], 0), e["D"]), np.uint8)
+        self._check(self.lib.sgm_debug_census_path(self.h, _ptr(left), _ptr(right), w, h, w, int(direction),
+                                                   _ptr(vol)))
+        return vol
+
+    def ocv_cost(self, left, right):
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        h, w = left.shape
+        e = effective_geometry(self.get_params(), w, h)
+        C = np.zeros((h, max(e["width1"], 0), e["D"]), np.int16)
+        self._check(self.lib.sgm_debug_ocv_cost(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(C)))
+        return C
+
+    def median3(self, disp):
+        d = np.ascontiguousarray(disp, np.int16).copy()
+        h, w = d.shape
+        self._check(self.lib.sgm_debug_median3(self.h, _ptr(d), w, h))
+        return d
+
+    def filter_speckles(self, disp, new_val, max_size, max_diff):
+        d = np.ascontiguousarray(disp, np.int16).copy()
+        h, w = d.shape
+        self._check(self.lib.sgm_debug_speckle(self.h, _ptr(d), w, h, new_val, max_size, max_diff))
+        return d
+
+
+def right_matcher_params(p):
+    """cv::ximgproc::createRightMatcher for a StereoSGBM: minD' = -(minD + D) + 1, same D /
+    block / P1 / P2 / mode / preFilterCap, uniqueness 0, disp12MaxDiff 1e6, no speckle filter
+    (reference calls it at matcherOpenCVSGBM.cpp:48)."""
+    return p.copy(min_disparity=-(p.min_disparity + p.num_disparities) + 1, uniqueness_ratio=0,
+                  disp12_max_diff=1000000, speckle_window_size=0)
+
+
+class MatcherHIPSGM:
+    """`MatcherHIPSGM : AbstractStereoMatcher` host mirror.
+
+    Same method names, argument meaning and error behaviour as the reference's
+    MatcherOpenCVSGBM (matcherOpenCVSGBM.{h,cpp}); compute delegated to libsgm_hip.so.
+    `mode` picks the engine mode (the reference's SGBM path never sets a mode, Q1, so the
+    OpenCV-compatible default is MODE_SGBM = 5 directions; env SGM_HIP_MODE overrides).
+    """
+
+    def __init__(self, param_file=" ", image_size=(0, 0), device=0, mode=None):
+        self.param_file = param_file
+        self.image_size = (0, 0)          # Q5: the base ctor ignores _image_size
+        self.downsample_scale = 1.0
+        self.min_disparity = 0
+        self.disparity_range = 64
+        self.window_size = 9
+        self.interpolate = False
+        self.left = None
+        self.right = None
+        self.disparity_lr = None
+        self.disparity_rl = None
+        if mode is None:
+            mode = int(os.environ.get("SGM_HIP_MODE", MODE_OCV_SGBM5))
+        self.device = device
+        self.mode = mode
+        self.init()
+
+    # --- AbstractStereoMatcher ----------------------------------------------------------
+    def init(self):
+        # cv::StereoSGBM::create(64, 9, 5) equivalent starting point (matcherOpenCVSGBM.cpp:14)
+        p = default_params(self.mode)
+        p.min_disparity, p.num_disparities, p.block_size = 64, 9, 5
+        p.p1 = p.p2 = p.uniqueness_ratio = p.disp12_max_diff = p.prefilter_cap = 0
+        p.speckle_window_size = p.speckle_range = 0
+        self.params = p
+        self._engine = None               # opened lazily at the first match (Q5 / §8b)
+
+    def setImages(self, left, right):
+        if left.shape != right.shape:
+            sys.stderr.write("Images MUST be the same resolution\n")
+            return
+        # scale 1 (the node always passes 1): cv::resize short-circuits to a copy
+        self.left = np.array(left, copy=True)
+        self.right = np.array(right, copy=True)
+        self.image_size = (self.left.shape[1], self.left.shape[0])
+
+    def setDownsampleScale(self, scale=1.0):
+        self.downsample_scale = scale
+
+    def setDisparityRange(self, disparity_range):
+        if disparity_range <= 0:
+            disparity_range = ((self.image_size[0] // 8) + 15) & -16
+        self.disparity_range = disparity_range
+        self.params.num_disparities = int(disparity_range)
+
+    def setWindowSize(self, window_size):
+        self.window_size = window_size
+        self.params.block_size = int(window_size)
+
+    def setInterpolation(self, enable):
+        self.interpolate = bool(enable)
+
+    def setMinDisparity(self, min_disparity):
+        self.min_disparity = min_disparity
+        self.params.min_disparity = int(min_disparity)
+
+    def setUniquenessRatio(self, ratio):
+        self.params.uniqueness_ratio = int(ratio)          # Q7: double in cfg -> int
+
+    def setSpeckleFilterWindow(self, window):
+        self.params.speckle_window_size = int(window)
+
+    def setSpeckleFilterRange(self, rng):
+        self.params.speckle_range = int(rng)
+
+    def setDisp12MaxDiff(self, diff):
+        self.params.disp12_max_diff = int(diff)
+
+    def setPreFilterCap(self, cap):
+        self.params.prefilter_cap = int(cap)
+
+    def setP1(self, p1):
+        self.params.p1 = int(p1)                           # OpenCV setP1(int): truncation
+
+    def setP2(self, p2):
+        self.params.p2 = int(p2)
+
+    def setTextureThreshold(self, threshold):              # not used by SGBM
+        pass
+
+    def setPreFilterSize(self, size):                      # not used by SGBM
+        pass
+
+    def setOcclusionDetection(self, enable):               # not used by SGBM
+        pass
+
+    def _engine_for(self):
+        if self._engine is None:
+            self._engine = Engine(self.device)
+        return self._engine
+
+    def _run(self, params, a, b):
+        eng = self._engine_for()
+        eng.set_params(params)
+        return eng.match(a, b)
+
+    def forwardMatch(self):
+        try:
+            disp = self._run(self.params, self.left, self.right)
+            if self.interpolate:
+                # Q3: the WLS output is discarded and disparity_rl replaces disparity_lr
+                self.backwardMatch()
+                disp = self.disparity_rl
+            self.disparity_lr = disp.astype(np.float32)
+            return 0
+        except Exception as e:  # mirrors the catch(cv::Exception&) -> -1
+            sys.stderr.write("Error in HIP SGM parameters\n%s\n" % e)
+            return -1
+
+    def backwardMatch(self):
+        self.disparity_rl = self._run(right_matcher_params(self.params), self.right, self.left)
+        return 0
+
+    def match(self):
+        code = self.forwardMatch()
+        if code == 0:
+            self.disparity_lr = self.disparity_lr.astype(np.float32)
+        return code
+
+    def getDisparity(self):
+        return None if self.disparity_lr is None else self.disparity_lr.copy()
+
+    def getBackDisparity(self):
+        return None if self.disparity_rl is None else self.disparity_rl.copy()
+
+    def getLeftImage(self):
+        return self.left
+
+    def getRighttImage(self):  # (sic) reference spelling, abstractStereoMatcher.h:71
+        return self.right
+
+
+# ---------------------------------------------------------------- node-level plumbing
+NODE_DEFAULTS = dict(stereo_algorithm=CV_StereoBM, min_disparity=9, disparity_range=64,
+                     correlation_window_size=15, uniqueness_ratio=15, texture_threshold=10,
+                     speckle_size=100, speckle_range=4, disp12MaxDiff=0, p1=200.0, p2=400.0,
+                     interp=False, prefilter_cap=31, prefilter_size=9)  # generate_disparity.cpp:90-112
+
+
+def update_matcher(matcher, cfg):
+    """updateMatcher() — generate_disparity.cpp:241-261 (disp12MaxDiff is NOT forwarded, Q1)."""
+    matcher.setDisparityRange(cfg["disparity_range"])
+    matcher.setWindowSize(cfg["correlation_window_size"])
+    matcher.setMinDisparity(cfg["min_disparity"])
+    matcher.setUniquenessRatio(int(cfg["uniqueness_ratio"]))
+    matcher.setSpeckleFilterRange(cfg["speckle_range"])
+    matcher.setSpeckleFilterWindow(cfg["speckle_size"])
+    matcher.setPreFilterCap(cfg["prefilter_cap"])
+    matcher.setP1(cfg["p1"])
+    matcher.setP2(cfg["p2"])
+    matcher.setTextureThreshold(cfg["texture_threshold"])
+    matcher.setPreFilterSize(cfg["prefilter_size"])
+    matcher.setInterpolation(cfg["interp"])
+
+
+def parameter_callback(config, state):
+    """parameterCallback() sanitising (generate_disparity.cpp:735-845) for the HIP entry.
+
+    `state` holds `first` (bool) and the node globals; returns the (possibly rewritten)
+    config like dynamic_reconfigure does."""
+    config = dict(config)
+    if state.get("first", True):
+        for k in NODE_DEFAULTS:
+            config[k] = state.get(k, NODE_DEFAULTS[k])
+        state["first"] = False
+        return config
+    config["prefilter_size"] |= 1
+    if config["stereo_algorithm"] in (CV_StereoBM, CV_StereoSGBM, CV_StereoBMCuda, CV_StereoBPCuda,
+                                      CV_StereoCSBPCuda, HIP_StereoSGM):
+        config["correlation_window_size"] |= 1
+        config["disparity_range"] = (config["disparity_range"] // 16) * 16
+    if config["stereo_algorithm"] == I3DR_StereoSGM and config["correlation_window_size"] > 17:
+        config["correlation_window_size"] = 17
+    for k in NODE_DEFAULTS:
+        state[k] = config[k]
+    return config
+
+
+def bgr2gray(img):
+    """cv::cvtColor(COLOR_BGR2GRAY) for 8U: fixed-point 14-bit coefficients, round half up."""
+    img = np.asarray(img)
+    if img.ndim == 2:
+        return img.astype(np.uint8, copy=True)
+    b, g, r = (img[..., i].astype(np.int32) for i in range(3))
+    return ((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14).astype(np.uint8)
+
+
+def stereo_match(matcher, left_mono, right_mono):
+    """stereo_match() — generate_disparity.cpp:334-368: empty result on failure."""
+    matcher.setDownsampleScale(1)
+    matcher.setImages(left_mono, right_mono)
+    code = matcher.match()
+    if code == 0:
+        return matcher.getDisparity()
+    sys.stderr.write(f"Exit code:{code}\nFailed to compute stereo match\nPlease check parameters are valid.\n")
+    return np.empty((0, 0), np.float32)
+
+
+def process_disparity(matcher, left_rect, right_rect, f, T, depth_min=0.0, depth_max=10.0):
+    """processDisparity() — generate_disparity.cpp:398-456. Returns the DisparityImage fields
+    or None when the match failed (the node returns -1 and publishes nothing)."""
+    disp = stereo_match(matcher, bgr2gray(left_rect), bgr2gray(right_rect))
+    if disp.size == 0:
+        return None
+    dmat = (disp.astype(np.float32) * np.float32(1.0 / 16)).astype(np.float32)
+    min_disp = np.float32(T * f / depth_max)
+    with np.errstate(divide="ignore"):
+        max_disp = np.float32(T * f / depth_min) if depth_min != 0 else np.float32(np.inf)  # Q8
+    dmat[dmat < min_disp] = MISSING_Z
+    dmat[dmat > max_disp] = MISSING_Z
+    return dict(image=dmat, f=f, T=T, min_disparity=float(min_disp), max_disparity=float(max_disp),
+                delta_d=1.0 / 16, height=dmat.shape[0], width=dmat.shape[1], encoding="32FC1",
+                step=dmat.shape[1] * 4)

@@ -1,0 +1,157 @@
+// post.hip — post filters of StereoSGBMImpl::compute:
+//   medianBlur(disp, disp, 3)                  -> k_median3 (int16, replicate border)
+//   filterSpeckles(disp, newVal, size, diff)   -> union-find connected components
+// Both are O(W*H) and bit-exact with oracle/sgm_oracle.c (sgmref_median3 /
+// sgmref_filter_speckles). Speckle regions are the 4-connected components of the graph
+// {p : disp(p) != newVal} with an edge p~q iff |disp(p) - disp(q)| <= maxDiff; a region
+// of <= maxSize pixels becomes newVal. Component membership is order-independent, so a
+// parallel union-find reproduces OpenCV's sequential flood fill exactly.
+#include "sgm_device.h"
+
+namespace sgm {
+
+__device__ __forceinline__ void sort2(int& a, int& b) { int t = min(a, b); b = max(a, b); a = t; }
+
+__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src, size_t sstride,
+                                                 int16_t* __restrict__ dst, size_t dstride, int W, int H)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    int p[9];
+    int n = 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++) {
+        const int16_t* r = src + (size_t)min(max(y + dy, 0), H - 1) * sstride;
+#pragma unroll
+        for (int dx = -1; dx <= 1; dx++) p[n++] = r[min(max(x + dx, 0), W - 1)];
+    }
+    // Paeth's 19-exchange median-of-9 network
+    sort2(p[1], p[2]); sort2(p[4], p[5]); sort2(p[7], p[8]);
+    sort2(p[0], p[1]); sort2(p[3], p[4]); sort2(p[6], p[7]);
+    sort2(p[1], p[2]); sort2(p[4], p[5]); sort2(p[7], p[8]);
+    sort2(p[0], p[3]); sort2(p[5], p[8]); sort2(p[4], p[7]);
+    sort2(p[3], p[6]); sort2(p[1], p[4]); sort2(p[2], p[5]);
+    sort2(p[4], p[7]); sort2(p[4], p[2]); sort2(p[6], p[4]);
+    sort2(p[4], p[2]);
+    dst[(size_t)y * dstride + x] = (int16_t)p[4];
+}
+
+hipError_t launch_median3(const int16_t* src, size_t sstride, int16_t* dst, size_t dstride, int W, int H,
+                          hipStream_t st)
+{
+    dim3 grid((W + 63) / 64, (H + 3) / 4);
+    hipLaunchKernelGGL(k_median3, grid, dim3(256), 0, st, src, sstride, dst, dstride, W, H);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- speckle filter ----
+// Invariant: lab[i] <= i and lab[i] is in i's component, so every chain ends at a root
+// and any (possibly stale) read is still a valid ancestor. Path halving writes go through
+// atomicMin so they can never overwrite a smaller link made concurrently on another XCD.
+__device__ __forceinline__ int uf_find_halve(int* __restrict__ lab, int x)
+{
+    int p = lab[x];
+    while (p != x) {
+        const int q = lab[p];
+        if (q != p) atomicMin(&lab[x], q);
+        x = p;
+        p = q;
+    }
+    return x;
+}
+
+// Read-only find (after the union phase has completed: a kernel boundary away).
+__device__ __forceinline__ int uf_root(const int* __restrict__ lab, int x)
+{
+    int p = lab[x];
+    while (p != x) { x = p; p = lab[x]; }
+    return x;
+}
+
+__device__ __forceinline__ void uf_union(int* __restrict__ lab, int a, int b)
+{
+    for (;;) {
+        a = uf_find_halve(lab, a);
+        b = uf_find_halve(lab, b);
+        if (a == b) return;
+        if (a < b) { int t = a; a = b; b = t; }          // link the larger root under the smaller
+        const int old = atomicMin(&lab[a], b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_spk_init(const int16_t* __restrict__ d, size_t stride, int W, int H,
+                                                  int newVal, int* __restrict__ lab, int* __restrict__ cnt)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H) return;
+    const int y = i / W, x = i - y * W;
+    lab[i] = d[(size_t)y * stride + x] != newVal ? i : -1;
+    cnt[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_spk_union(const int16_t* __restrict__ d, size_t stride, int W, int H,
+                                                   int newVal, int maxDiff, int* __restrict__ lab)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H) return;
+    const int y = i / W, x = i - y * W;
+    const int v = d[(size_t)y * stride + x];
+    if (v == newVal) return;
+    if (x + 1 < W) {
+        const int q = d[(size_t)y * stride + x + 1];
+        if (q != newVal && abs(v - q) <= maxDiff) uf_union(lab, i, i + 1);
+    }
+    if (y + 1 < H) {
+        const int q = d[(size_t)(y + 1) * stride + x];
+        if (q != newVal && abs(v - q) <= maxDiff) uf_union(lab, i, i + W);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_spk_count(int W, int H, const int* __restrict__ lab, int* __restrict__ cnt)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H || lab[i] < 0) return;
+    atomicAdd(&cnt[uf_root(lab, i)], 1);
+}
+
+__global__ __launch_bounds__(256) void k_spk_apply(int16_t* __restrict__ d, size_t stride, int W, int H, int newVal,
+                                                   int maxSize, const int* __restrict__ lab,
+                                                   const int* __restrict__ cnt)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W * H) return;
+    if (lab[i] < 0) return;
+    if (cnt[uf_root(lab, i)] <= maxSize) {
+        const int y = i / W, x = i - y * W;
+        d[(size_t)y * stride + x] = (int16_t)newVal;
+    }
+}
+
+hipError_t launch_speckle(int16_t* d, size_t stride, int W, int H, int newVal, int maxSize, int maxDiff,
+                          int* lab, int* cnt, hipStream_t st)
+{
+    const int n = W * H;
+    dim3 grid((n + 255) / 256), block(256);
+    hipLaunchKernelGGL(k_spk_init, grid, block, 0, st, d, stride, W, H, newVal, lab, cnt);
+    hipLaunchKernelGGL(k_spk_union, grid, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
+    hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, lab, cnt);
+    hipLaunchKernelGGL(k_spk_apply, grid, block, 0, st, d, stride, W, H, newVal, maxSize, lab, cnt);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_fill16(int16_t* __restrict__ d, size_t stride, int W, int H, int v)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x < W && y < H) d[(size_t)y * stride + x] = (int16_t)v;
+}
+
+hipError_t launch_fill16(int16_t* d, size_t stride, int W, int H, int v, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_fill16, dim3((W + 255) / 256, H), dim3(256), 0, st, d, stride, W, H, v);
+    return hipGetLastError();
+}
+
+}  // namespace sgm

@@ -1,0 +1,632 @@
+// sgm_api.cpp — C-ABI of libsgm_hip.so (include/sgm_hip.h).
+//
+// The handle owns one HIP stream and one device workspace on its device. Geometry-
+// dependent buffers are (re)allocated lazily at the first match and whenever W, H, D or
+// the mode change — mirroring the reference, which constructs its matchers lazily at the
+// first frame (generate_disparity.cpp:342-346) and never frees them.
+// A per-handle mutex serialises set_params against match (the reference's only locking
+// matcher does the same: I3DRSGM.cpp:152, :635).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sgm_device.h"
+#include "sgm_hip.h"
+
+namespace sgm {
+hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
+hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_census_final(const uint64_t*, const uint64_t*, const uint8_t*, size_t, const Geom&, int16_t*,
+                               size_t, hipStream_t);
+hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
+hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
+hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
+hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
+                           hipStream_t);
+hipError_t launch_ocv_paths(const int16_t*, int16_t*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_ocv_wta(const int16_t*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
+}  // namespace sgm
+
+using sgm::Geom;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+// effective parameters — identical rules to the oracle (oracle/sgm_oracle.c effective())
+int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
+{
+    if (W <= 0 || H <= 0) { err = "image size must be positive"; return SGM_ERR_ARG; }
+    if (W > 32767 || H > 32767) { err = "image larger than 32767 pixels"; return SGM_ERR_UNSUPPORTED; }
+    if (p.mode < SGM_MODE_OCV_SGBM5 || p.mode > SGM_MODE_CENSUS8) { err = "unknown mode"; return SGM_ERR_PARAM; }
+    if (p.num_disparities <= 0 || p.num_disparities % 16 != 0) {
+        err = "numDisparities must be a positive multiple of 16 (OpenCV: CV_Assert(D % 16 == 0))";
+        return SGM_ERR_PARAM;
+    }
+    if (p.num_disparities > 512) { err = "numDisparities > 512 is not supported by this build"; return SGM_ERR_UNSUPPORTED; }
+    g = Geom{};
+    g.W = W; g.H = H;
+    g.minD = p.min_disparity; g.D = p.num_disparities;
+    const int maxD = g.minD + g.D;
+    if (p.mode == SGM_MODE_CENSUS8) {
+        g.P1 = p.p1 > 0 ? p.p1 : 10;
+        g.P2 = std::max(p.p2 > 0 ? p.p2 : 120, g.P1 + 1);
+        if (g.P2 > 193) g.P2 = 193;                   // u8 path costs: 62 + P2 <= 255
+        if (g.P1 >= g.P2) g.P1 = g.P2 - 1;
+        g.subpix = p.subpixel != 0; g.lr = p.lr_check != 0;
+        g.SW2 = 4; g.SH2 = 3; g.ftzero = 0;
+    } else {
+        const int sw = p.block_size > 0 ? p.block_size : 5;
+        g.SW2 = sw / 2; g.SH2 = sw / 2;
+        g.ftzero = std::max(p.prefilter_cap, 15) | 1;
+        g.P1 = p.p1 > 0 ? p.p1 : 2;
+        g.P2 = std::max(p.p2 > 0 ? p.p2 : 5, g.P1 + 1);
+        g.subpix = 1; g.lr = 1;
+    }
+    g.uniq = p.uniqueness_ratio >= 0 ? p.uniqueness_ratio : 10;
+    g.disp12 = p.disp12_max_diff > 0 ? p.disp12_max_diff : 1;
+    g.minX1 = std::max(maxD, 0);
+    g.maxX1 = W + std::min(g.minD, 0);
+    g.width1 = g.maxX1 - g.minX1;
+    g.invalid = (g.minD - 1) * 16;
+    return SGM_OK;
+}
+
+bool use_median(const sgm_params& p) { return p.mode != SGM_MODE_CENSUS8 || p.median != 0; }
+
+struct Workspace {
+    void* base = nullptr;
+    size_t size = 0;
+};
+
+}  // namespace
+
+struct sgm_handle {
+    int device = 0;
+    sgm_params params{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::mutex mu;
+    Workspace ws;
+    uint8_t* pin = nullptr;      // pinned host staging
+    size_t pin_size = 0;
+    bool profiling = false;
+    struct ProfRec { hipEvent_t ev[SGM_MAX_STAGES + 1]; int n; };
+    std::vector<ProfRec> prof;     // event pool, one record per profiled match
+    size_t prof_used = 0;
+    int nstages = 0;
+    const char* stage_name[SGM_MAX_STAGES] = {};
+    double stage_bytes[SGM_MAX_STAGES] = {};
+    std::vector<sgm_handle*> sub;  // per-device handles for sgm_match_batch
+};
+
+namespace {
+
+int fail(sgm_handle* h, int code, const std::string& msg)
+{
+    if (h) h->err = msg;
+    return code;
+}
+
+int hip_fail(sgm_handle* h, hipError_t e, const char* where)
+{
+    return fail(h, SGM_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, where)                                   \
+    do {                                                       \
+        hipError_t e_ = (expr);                                \
+        if (e_ != hipSuccess) return hip_fail(h, e_, where);   \
+    } while (0)
+
+int ensure_stream(sgm_handle* h)
+{
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+    return SGM_OK;
+}
+
+// Next free event record of the profiling pool (grows on demand; events are reused after a
+// re-enable). Returns nullptr when profiling is off.
+sgm_handle::ProfRec* next_prof(sgm_handle* h)
+{
+    if (!h->profiling) return nullptr;
+    if (h->prof_used == h->prof.size()) {
+        sgm_handle::ProfRec r{};
+        for (int i = 0; i <= SGM_MAX_STAGES; i++)
+            if (hipEventCreate(&r.ev[i]) != hipSuccess) return nullptr;
+        h->prof.push_back(r);
+    }
+    sgm_handle::ProfRec* r = &h->prof[h->prof_used++];
+    r->n = 0;
+    return r;
+}
+
+int ensure_ws(sgm_handle* h, size_t bytes)
+{
+    if (h->ws.size >= bytes) return SGM_OK;
+    if (h->ws.base) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipFree(h->ws.base);
+        h->ws.base = nullptr;
+        h->ws.size = 0;
+    }
+    hipError_t e = hipMalloc(&h->ws.base, bytes);
+    if (e != hipSuccess) {
+        h->ws.base = nullptr;
+        return fail(h, SGM_ERR_ALLOC, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
+    }
+    h->ws.size = bytes;
+    return SGM_OK;
+}
+
+int ensure_pin(sgm_handle* h, size_t bytes)
+{
+    if (h->pin_size >= bytes) return SGM_OK;
+    if (h->pin) { (void)hipStreamSynchronize(h->stream); (void)hipHostFree(h->pin); h->pin = nullptr; h->pin_size = 0; }
+    hipError_t e = hipHostMalloc((void**)&h->pin, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) { h->pin = nullptr; return fail(h, SGM_ERR_ALLOC, "hipHostMalloc staging"); }
+    h->pin_size = bytes;
+    return SGM_OK;
+}
+
+// Workspace carve-up for one geometry. Offsets are 256-B aligned.
+struct Layout {
+    size_t cL = 0, cR = 0, vols = 0, vol_bytes = 0;       // census
+    size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovol_elems = 0;  // ocv
+    size_t tmp = 0, lab = 0, cnt = 0;                      // post
+    size_t inL = 0, inR = 0, out = 0;                      // host-API staging
+    size_t total = 0;
+};
+
+Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
+{
+    Layout l;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
+    const size_t WH = (size_t)g.W * g.H;
+    const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
+    if (p.mode == SGM_MODE_CENSUS8) {
+        l.cL = take(WH * 8);
+        l.cR = take(WH * 8);
+        l.vol_bytes = align_up(cells);
+        l.vols = take(l.vol_bytes * 7);
+    } else {
+        l.planes = take(WH * 4);
+        l.bufA = take(cells * 2);
+        l.bufB = take(cells * 2);
+        l.ovol_elems = align_up(cells * 2) / 2;
+        l.ovols = take(l.ovol_elems * 2 * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5));
+    }
+    l.tmp = take(WH * 2);
+    if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
+    if (host_io) { l.inL = take(WH); l.inR = take(WH); l.out = take(WH * 2); }
+    l.total = off;
+    return l;
+}
+
+struct StageRec {
+    sgm_handle* h;
+    sgm_handle::ProfRec* r = nullptr;
+    int n = 0;
+    void begin(const char* name, double bytes)
+    {
+        if (n < SGM_MAX_STAGES) {
+            h->stage_name[n] = name;
+            h->stage_bytes[n] = bytes;
+            if (r) (void)hipEventRecord(r->ev[n], h->stream);
+        }
+        n++;
+    }
+    void end()
+    {
+        h->nstages = std::min(n, SGM_MAX_STAGES);
+        if (r) {
+            (void)hipEventRecord(r->ev[h->nstages], h->stream);
+            r->n = h->nstages;
+        }
+    }
+};
+
+// Runs the whole pipeline on device buffers, asynchronously on h->stream.
+int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
+                 int16_t* dOut, size_t out_stride)
+{
+    const sgm_params& p = h->params;
+    char* ws = (char*)h->ws.base;
+    hipStream_t st = h->stream;
+    const bool med = use_median(p);
+    const bool spk = p.speckle_window_size > 0;
+    int16_t* tmp = (int16_t*)(ws + l.tmp);
+    // the disparity producer writes to `tmp` when a median follows, else directly to dOut
+    int16_t* dst = med ? tmp : dOut;
+    const size_t dst_stride = med ? (size_t)g.W : out_stride;
+    const double WH = (double)g.W * g.H;
+    const double cells = (double)std::max(g.width1, 0) * g.H * g.D;
+    StageRec rec{h, next_prof(h)};
+    h->nstages = 0;
+    if (g.width1 <= 0) {
+        rec.begin("fill_invalid", 2 * WH);
+        HIP_TRY(sgm::launch_fill16(dst, dst_stride, g.W, g.H, g.invalid, st), "fill");
+    } else if (p.mode == SGM_MODE_CENSUS8) {
+        uint64_t* cL = (uint64_t*)(ws + l.cL);
+        uint64_t* cR = (uint64_t*)(ws + l.cR);
+        uint8_t* vols = (uint8_t*)(ws + l.vols);
+        rec.begin("census", 2 * WH + 16 * WH);
+        HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
+        rec.begin("paths7", 7 * cells);
+        HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, -1, st), "paths");
+        rec.begin("final_wta_lr", 7 * cells + 2 * WH);
+        HIP_TRY(sgm::launch_census_final(cL, cR, vols, l.vol_bytes, g, dst, dst_stride, st), "final");
+    } else {
+        const int fullDP = p.mode == SGM_MODE_OCV_HH8;
+        const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
+        const int ndir = fullDP ? 8 : 5;
+        int16_t* A = (int16_t*)(ws + l.bufA);
+        int16_t* B = (int16_t*)(ws + l.bufB);
+        int16_t* V = (int16_t*)(ws + l.ovols);
+        rec.begin("ocv_cost", 2 * WH + 2 * cells);
+        HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, g, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
+        rec.begin("ocv_paths", 2 * cells * (ndir + 1));
+        HIP_TRY(sgm::launch_ocv_paths(A, V, l.ovol_elems, g, mask, st), "ocv_paths");
+        rec.begin("ocv_wta_lr", 2 * cells * ndir + 2 * WH);
+        HIP_TRY(sgm::launch_ocv_wta(V, l.ovol_elems, ndir, g, dst, dst_stride, st), "ocv_wta");
+    }
+    if (med) {
+        rec.begin("median3", 4 * WH);
+        HIP_TRY(sgm::launch_median3(tmp, g.W, dOut, out_stride, g.W, g.H, st), "median3");
+    }
+    if (spk) {
+        rec.begin("speckle", 14 * WH);
+        HIP_TRY(sgm::launch_speckle(dOut, out_stride, g.W, g.H, g.invalid, p.speckle_window_size,
+                                    16 * p.speckle_range, (int*)(ws + l.lab), (int*)(ws + l.cnt), st),
+                "speckle");
+    }
+    rec.end();
+    return SGM_OK;
+}
+
+int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l)
+{
+    int rc = make_geom(h->params, W, H, g, h->err);
+    if (rc) return rc;
+    if ((rc = ensure_stream(h))) return rc;
+    l = make_layout(h->params, g, host_io);
+    return ensure_ws(h, l.total);
+}
+
+}  // namespace
+
+// ==================================================================================== C-ABI
+extern "C" {
+
+int sgm_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void sgm_default_params(sgm_params* p, int mode)
+{
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->mode = mode;
+    if (mode == SGM_MODE_CENSUS8) {
+        p->min_disparity = 0; p->num_disparities = 128; p->p1 = 10; p->p2 = 120;
+        p->uniqueness_ratio = 5; p->disp12_max_diff = 1; p->subpixel = 1; p->lr_check = 1; p->median = 0;
+    } else {
+        // generate_disparity.cpp:100-112 node defaults
+        p->min_disparity = 9; p->num_disparities = 64; p->block_size = 15; p->p1 = 200; p->p2 = 400;
+        p->uniqueness_ratio = 15; p->disp12_max_diff = 0; p->prefilter_cap = 31; p->speckle_window_size = 100;
+        p->speckle_range = 4; p->subpixel = 1; p->lr_check = 1; p->median = 1;
+    }
+}
+
+int sgm_create(sgm_handle** out, int device)
+{
+    if (!out) return SGM_ERR_ARG;
+    *out = nullptr;
+    const int n = sgm_device_count();
+    if (device < 0 || device >= n) return SGM_ERR_DEVICE;
+    sgm_handle* h = new (std::nothrow) sgm_handle();
+    if (!h) return SGM_ERR_ALLOC;
+    h->device = device;
+    sgm_default_params(&h->params, SGM_MODE_CENSUS8);
+    *out = h;
+    return SGM_OK;
+}
+
+void sgm_destroy(sgm_handle* h)
+{
+    if (!h) return;
+    for (sgm_handle* s : h->sub) sgm_destroy(s);
+    if (hipSetDevice(h->device) == hipSuccess) {
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        if (h->ws.base) (void)hipFree(h->ws.base);
+        if (h->pin) (void)hipHostFree(h->pin);
+        for (auto& r : h->prof)
+            for (int i = 0; i <= SGM_MAX_STAGES; i++) (void)hipEventDestroy(r.ev[i]);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+}
+
+int sgm_set_params(sgm_handle* h, const sgm_params* p)
+{
+    if (!h || !p) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->params = *p;
+    return SGM_OK;
+}
+
+int sgm_get_params(const sgm_handle* h, sgm_params* p)
+{
+    if (!h || !p) return SGM_ERR_ARG;
+    *p = h->params;
+    return SGM_OK;
+}
+
+int sgm_check_params(const sgm_params* p, int width, int height)
+{
+    if (!p) return SGM_ERR_ARG;
+    Geom g;
+    std::string err;
+    return make_geom(*p, width, height, g, err);
+}
+
+const char* sgm_last_error(const sgm_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int sgm_match_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, int H, size_t stride, int16_t* dOut,
+                     size_t out_stride, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!dL || !dR || !dOut || stride < (size_t)W || out_stride < (size_t)W) return fail(h, SGM_ERR_ARG, "bad buffers");
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, false, g, l);
+    if (rc) return rc;
+    hipStream_t own = h->stream;
+    if (stream) h->stream = (hipStream_t)stream;
+    rc = run_pipeline(h, l, g, dL, dR, stride, dOut, out_stride);
+    h->stream = own;
+    return rc;
+}
+
+int sgm_synchronize(sgm_handle* h)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!h->stream) return SGM_OK;
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    HIP_TRY(hipStreamSynchronize(h->stream), "hipStreamSynchronize");
+    return SGM_OK;
+}
+
+int sgm_match(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int16_t* disp,
+              size_t out_stride)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W)
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, true, g, l);
+    if (rc) return rc;
+    const size_t WH = (size_t)W * H;
+    if ((rc = ensure_pin(h, WH * 4))) return rc;
+    char* ws = (char*)h->ws.base;
+    // pack rows into pinned staging (one H2D copy per image)
+    for (int y = 0; y < H; y++) {
+        std::memcpy(h->pin + (size_t)y * W, L + (size_t)y * stride, W);
+        std::memcpy(h->pin + WH + (size_t)y * W, R + (size_t)y * stride, W);
+    }
+    HIP_TRY(hipMemcpyAsync(ws + l.inL, h->pin, WH, hipMemcpyHostToDevice, h->stream), "H2D L");
+    HIP_TRY(hipMemcpyAsync(ws + l.inR, h->pin + WH, WH, hipMemcpyHostToDevice, h->stream), "H2D R");
+    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W,
+                      (int16_t*)(ws + l.out), W);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(h->pin, ws + l.out, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    const int16_t* src = (const int16_t*)h->pin;
+    for (int y = 0; y < H; y++) std::memcpy(disp + (size_t)y * out_stride, src + (size_t)y * W, 2 * (size_t)W);
+    return SGM_OK;
+}
+
+int sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights, int n_frames, int W,
+                    int H, size_t stride, int16_t* const* disps, size_t out_stride, const int* devices, int n_dev)
+{
+    if (!h || !lefts || !rights || !disps || n_frames < 0) return SGM_ERR_ARG;
+    std::vector<int> devs;
+    if (!devices || n_dev <= 0) {
+        const int n = sgm_device_count();
+        for (int i = 0; i < n; i++) devs.push_back(i);
+    } else {
+        devs.assign(devices, devices + n_dev);
+    }
+    if (devs.empty()) return fail(h, SGM_ERR_DEVICE, "no HIP device");
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        while (h->sub.size() < devs.size()) h->sub.push_back(nullptr);
+        for (size_t i = 0; i < devs.size(); i++) {
+            if (h->sub[i] && h->sub[i]->device != devs[i]) { sgm_destroy(h->sub[i]); h->sub[i] = nullptr; }
+            if (!h->sub[i]) {
+                int rc = sgm_create(&h->sub[i], devs[i]);
+                if (rc) return fail(h, rc, "cannot open device " + std::to_string(devs[i]));
+            }
+            h->sub[i]->params = h->params;
+        }
+    }
+    std::vector<int> rcs(devs.size(), SGM_OK);
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < devs.size(); t++) {
+        th.emplace_back([&, t]() {
+            for (int i = (int)t; i < n_frames; i += (int)devs.size()) {
+                int rc = sgm_match(h->sub[t], lefts[i], rights[i], W, H, stride, disps[i], out_stride);
+                if (rc) { rcs[t] = rc; return; }
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (size_t t = 0; t < devs.size(); t++)
+        if (rcs[t]) return fail(h, rcs[t], std::string("device ") + std::to_string(devs[t]) + ": " + h->sub[t]->err);
+    return SGM_OK;
+}
+
+int sgm_set_profiling(sgm_handle* h, int enable)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->profiling = enable != 0;
+    h->prof_used = 0;
+    return SGM_OK;
+}
+
+int sgm_profiled_matches(const sgm_handle* h) { return h ? (int)h->prof_used : 0; }
+
+int sgm_get_stage_times(sgm_handle* h, float* ms, int max)
+{
+    if (!h || !ms) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->prof_used == 0) return 0;
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    const sgm_handle::ProfRec& last = h->prof[h->prof_used - 1];
+    HIP_TRY(hipEventSynchronize(last.ev[last.n]), "hipEventSynchronize");
+    const int n = std::min(last.n, max);
+    std::vector<double> acc(n, 0.0);
+    int cnt = 0;
+    for (size_t k = 0; k < h->prof_used; k++) {
+        const sgm_handle::ProfRec& r = h->prof[k];
+        if (r.n != last.n) continue;
+        for (int i = 0; i < n; i++) {
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, r.ev[i], r.ev[i + 1]), "hipEventElapsedTime");
+            acc[i] += t;
+        }
+        cnt++;
+    }
+    for (int i = 0; i < n; i++) ms[i] = (float)(acc[i] / std::max(cnt, 1));
+    return n;
+}
+
+const char* sgm_stage_name(const sgm_handle* h, int i)
+{
+    if (!h || i < 0 || i >= h->nstages) return "";
+    return h->stage_name[i];
+}
+
+double sgm_stage_bytes(const sgm_handle* h, int i)
+{
+    if (!h || i < 0 || i >= h->nstages) return 0.0;
+    return h->stage_bytes[i];
+}
+
+// ------------------------------------------------------------------ stage entry points
+int sgm_debug_census(sgm_handle* h, const uint8_t* img, int W, int H, size_t stride, uint64_t* out)
+{
+    if (!h || !img || !out || W <= 0 || H <= 0 || stride < (size_t)W) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    const size_t WH = (size_t)W * H;
+    if ((rc = ensure_ws(h, align_up(WH) + WH * 8))) return rc;
+    char* ws = (char*)h->ws.base;
+    HIP_TRY(hipMemcpy2DAsync(ws, W, img, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
+    HIP_TRY(sgm::launch_census((const uint8_t*)ws, nullptr, W, W, H, (uint64_t*)(ws + align_up(WH)), nullptr,
+                               h->stream), "census");
+    HIP_TRY(hipMemcpyAsync(out, ws + align_up(WH), WH * 8, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SGM_OK;
+}
+
+int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int dir,
+                          uint8_t* vol)
+{
+    if (!h || !L || !R || !vol || dir < 0 || dir > 6) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->params.mode != SGM_MODE_CENSUS8) return fail(h, SGM_ERR_PARAM, "census mode required");
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, true, g, l);
+    if (rc) return rc;
+    if (g.width1 <= 0) return SGM_OK;
+    char* ws = (char*)h->ws.base;
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
+    uint64_t* cL = (uint64_t*)(ws + l.cL);
+    uint64_t* cR = (uint64_t*)(ws + l.cR);
+    uint8_t* vols = (uint8_t*)(ws + l.vols);
+    HIP_TRY(sgm::launch_census((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, W, H, cL, cR, h->stream),
+            "census");
+    HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, dir, h->stream), "paths");
+    const size_t cells = (size_t)g.width1 * g.H * g.D;
+    HIP_TRY(hipMemcpyAsync(vol, vols + (size_t)dir * l.vol_bytes, cells, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SGM_OK;
+}
+
+int sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int16_t* cost)
+{
+    if (!h || !L || !R || !cost) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->params.mode == SGM_MODE_CENSUS8) return fail(h, SGM_ERR_PARAM, "OCV mode required");
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, true, g, l);
+    if (rc) return rc;
+    if (g.width1 <= 0) return SGM_OK;
+    char* ws = (char*)h->ws.base;
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
+    int16_t* A = (int16_t*)(ws + l.bufA);
+    HIP_TRY(sgm::launch_ocv_cost((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, g,
+                                 h->params.mode == SGM_MODE_OCV_HH8, (uint8_t*)(ws + l.planes), A,
+                                 (int16_t*)(ws + l.bufB), h->stream), "ocv_cost");
+    const size_t cells = (size_t)g.width1 * g.H * g.D;
+    HIP_TRY(hipMemcpyAsync(cost, A, cells * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SGM_OK;
+}
+
+static int debug_post(sgm_handle* h, int16_t* disp, int W, int H, int which, int nv, int ms, int md)
+{
+    if (!h || !disp || W <= 0 || H <= 0) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    const size_t WH = (size_t)W * H;
+    if ((rc = ensure_ws(h, align_up(WH * 2) * 2 + align_up(WH * 4) * 2))) return rc;
+    char* ws = (char*)h->ws.base;
+    int16_t* a = (int16_t*)ws;
+    int16_t* b = (int16_t*)(ws + align_up(WH * 2));
+    int* lab = (int*)(ws + 2 * align_up(WH * 2));
+    int* cnt = (int*)(ws + 2 * align_up(WH * 2) + align_up(WH * 4));
+    HIP_TRY(hipMemcpyAsync(a, disp, WH * 2, hipMemcpyHostToDevice, h->stream), "H2D");
+    if (which == 0) {
+        HIP_TRY(sgm::launch_median3(a, W, b, W, W, H, h->stream), "median3");
+        HIP_TRY(hipMemcpyAsync(disp, b, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    } else {
+        HIP_TRY(sgm::launch_speckle(a, W, W, H, nv, ms, md, lab, cnt, h->stream), "speckle");
+        HIP_TRY(hipMemcpyAsync(disp, a, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SGM_OK;
+}
+
+int sgm_debug_median3(sgm_handle* h, int16_t* disp, int W, int H) { return debug_post(h, disp, W, H, 0, 0, 0, 0); }
+
+int sgm_debug_speckle(sgm_handle* h, int16_t* disp, int W, int H, int new_val, int max_size, int max_diff)
+{
+    return debug_post(h, disp, W, H, 1, new_val, max_size, max_diff);
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// hip_sgm_core.cpp — see hip_sgm_core.h.
+#include "hip_sgm_core.h"
+
+#include <cstdlib>
+#include <iostream>
+
+namespace sgm_hip {
+
+MatcherCore::MatcherCore(int device, int mode) : device_(device)
+{
+    if (mode < 0) {
+        const char* env = std::getenv("SGM_HIP_MODE");
+        mode = env ? std::atoi(env) : SGM_MODE_OCV_SGBM5;
+    }
+    sgm_default_params(&params_, mode);
+    // cv::StereoSGBM::create(64, 9, 5) (matcherOpenCVSGBM.cpp:14): overwritten by the setters
+    params_.min_disparity = 64;
+    params_.num_disparities = 9;
+    params_.block_size = 5;
+    params_.p1 = params_.p2 = params_.uniqueness_ratio = params_.disp12_max_diff = 0;
+    params_.prefilter_cap = params_.speckle_window_size = params_.speckle_range = 0;
+}
+
+MatcherCore::~MatcherCore() { sgm_destroy(handle_); }
+
+void MatcherCore::setDisparityRange(int r, int image_width)
+{
+    r = r > 0 ? r : ((image_width / 8) + 15) & -16;
+    params_.num_disparities = r;
+}
+void MatcherCore::setWindowSize(int w) { params_.block_size = w; }
+void MatcherCore::setMinDisparity(int d) { params_.min_disparity = d; }
+void MatcherCore::setUniquenessRatio(int r) { params_.uniqueness_ratio = r; }
+void MatcherCore::setSpeckleFilterWindow(int w) { params_.speckle_window_size = w; }
+void MatcherCore::setSpeckleFilterRange(int r) { params_.speckle_range = r; }
+void MatcherCore::setDisp12MaxDiff(int d) { params_.disp12_max_diff = d; }
+void MatcherCore::setPreFilterCap(int c) { params_.prefilter_cap = c; }
+void MatcherCore::setP1(float p1) { params_.p1 = (int)p1; }
+void MatcherCore::setP2(float p2) { params_.p2 = (int)p2; }
+void MatcherCore::setInterpolation(bool e) { interpolate_ = e; }
+void MatcherCore::setMode(int m) { params_.mode = m; }
+
+sgm_params MatcherCore::rightMatcherParams(const sgm_params& p)
+{
+    sgm_params r = p;
+    r.min_disparity = -(p.min_disparity + p.num_disparities) + 1;
+    r.uniqueness_ratio = 0;
+    r.disp12_max_diff = 1000000;
+    r.speckle_window_size = 0;
+    return r;
+}
+
+int MatcherCore::run(const sgm_params& p, const uint8_t* a, const uint8_t* b, int w, int h, size_t stride, float* out,
+                     size_t out_stride)
+{
+    int rc = SGM_OK;
+    if (!handle_) rc = sgm_create(&handle_, device_);
+    if (rc == SGM_OK) rc = sgm_set_params(handle_, &p);
+    if (rc == SGM_OK) {
+        buf_.resize((size_t)w * h);
+        rc = sgm_match(handle_, a, b, w, h, stride, buf_.data(), (size_t)w);
+    }
+    if (rc != SGM_OK) {
+        err_ = handle_ ? sgm_last_error(handle_) : "no HIP device";
+        std::cerr << "Error in HIP SGM parameters" << std::endl << err_ << " (status " << rc << ")" << std::endl;
+        return -1;
+    }
+    for (int y = 0; y < h; y++) {
+        const int16_t* s = buf_.data() + (size_t)y * w;
+        float* d = out + (size_t)y * out_stride;
+        for (int x = 0; x < w; x++) d[x] = (float)s[x];   // convertTo(CV_32FC1): exact
+    }
+    return 0;
+}
+
+int MatcherCore::forwardMatch(const uint8_t* left, const uint8_t* right, int w, int h, size_t stride, float* out,
+                              size_t out_stride)
+{
+    if (interpolate_)  // Q3: WLS output discarded, right-view disparity returned
+        return backwardMatch(left, right, w, h, stride, out, out_stride);
+    return run(params_, left, right, w, h, stride, out, out_stride);
+}
+
+int MatcherCore::backwardMatch(const uint8_t* left, const uint8_t* right, int w, int h, size_t stride, float* out,
+                               size_t out_stride)
+{
+    return run(rightMatcherParams(params_), right, left, w, h, stride, out, out_stride);
+}
+
+}  // namespace sgm_hip

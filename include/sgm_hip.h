@@ -1,0 +1,156 @@
+/*
+ * sgm_hip.h — C-ABI of the MI355X-native Semi-Global Matching engine (libsgm_hip.so).
+ *
+ * This is the drop-in boundary for the reference's stereo-matcher plugin surface.
+ * It replaces the work that `MatcherOpenCVSGBM::forwardMatch` delegates to
+ * `cv::StereoSGBM::compute` (reference: src/stereoMatcher/matcherOpenCVSGBM.cpp:17-44,
+ * call at :21) and is called from the plugin adapter `MatcherHIPSGM`
+ * (i3dr_stereo_camera-ros_amd/plugin/matcherHIPSGM.{h,cpp}), a subclass of the
+ * reference's `AbstractStereoMatcher` (include/stereoMatcher/abstractStereoMatcher.h:12-92).
+ *
+ * Plain C types only: pointers, sizes, ints. No torch / OpenCV / HIP types in signatures
+ * (streams are passed as `void*` = hipStream_t).
+ *
+ * Output contract (identical to the reference's SGBM path, abstractStereoMatcher.cpp:44-53,
+ * generate_disparity.cpp:403-436): int16 disparity in 1/16-pixel fixed point
+ * (OpenCV DISP_SCALE = 16); invalid pixels = (min_disparity - 1) * 16; columns outside
+ * [max(maxD,0), W + min(minD,0)) are invalid.
+ *
+ * Error convention (reference: matcherOpenCVSGBM.cpp:37-43 returns -1 on cv::Exception;
+ * generate_disparity.cpp:355-365 logs and publishes nothing): every call returns an int
+ * status, 0 = OK, < 0 = error class below; `sgm_last_error()` gives the text. The adapter
+ * maps any non-zero status to -1, exactly like the OpenCV wrapper.
+ */
+#ifndef SGM_HIP_H
+#define SGM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define SGM_OK                0
+#define SGM_ERR_ARG          -1   /* null pointer, bad size / stride                      */
+#define SGM_ERR_PARAM        -2   /* invalid matcher parameters (e.g. D % 16 != 0)       */
+#define SGM_ERR_DEVICE       -3   /* no HIP device / HIP runtime failure                  */
+#define SGM_ERR_ALLOC        -4   /* device / host allocation failure                     */
+#define SGM_ERR_UNSUPPORTED  -5   /* parameter combination this build does not implement */
+
+/* ---- matching modes ---------------------------------------------------------------- */
+/* OpenCV-compatible modes: Birchfield-Tomasi cost on the Sobel-prefiltered + raw image,
+ * SAD block aggregation, int16 path costs. Bit-exact with the CPU oracle's restatement of
+ * cv::StereoSGBM (oracle/sgm_oracle.c).                                                   */
+#define SGM_MODE_OCV_SGBM5    0   /* cv::StereoSGBM::MODE_SGBM: 5 directions (reference default, Q1) */
+#define SGM_MODE_OCV_HH8      1   /* cv::StereoSGBM::MODE_HH: 8 directions (cfg `fullDP`)             */
+/* North-star mode: 9x7 census, Hamming cost, 8 directions, u8 path costs, u16 sums.       */
+#define SGM_MODE_CENSUS8      2
+
+/* Parameter block. Field names follow the reference's setters
+ * (abstractStereoMatcher.h:27-48) and cfg/i3DR_Disparity.cfg:21-39.                      */
+typedef struct sgm_params {
+    int mode;                 /* SGM_MODE_*                                               */
+    int min_disparity;        /* setMinDisparity                  (cfg min_disparity)     */
+    int num_disparities;      /* setDisparityRange, multiple of 16 (cfg disparity_range)  */
+    int block_size;           /* setWindowSize: OCV SAD window (cfg correlation_window_size); census: ignored */
+    int p1;                   /* setP1 (float in the reference API, truncated like OpenCV's int setter) */
+    int p2;                   /* setP2                                                    */
+    int uniqueness_ratio;     /* setUniquenessRatio (percent)                             */
+    int disp12_max_diff;      /* setDisp12MaxDiff (<=0 -> 1, as OpenCV SGBM)              */
+    int prefilter_cap;        /* setPreFilterCap (OCV modes)                              */
+    int speckle_window_size;  /* setSpeckleFilterWindow (0 = speckle filter off)          */
+    int speckle_range;        /* setSpeckleFilterRange (max diff in pixels; x16 internally) */
+    int subpixel;             /* census: parabolic 1/16 interpolation on/off (OCV: always on) */
+    int lr_check;             /* census: left-right (disp2) check on/off (OCV: always on)     */
+    int median;               /* census: 3x3 median post-filter on/off (OCV: always on)       */
+} sgm_params;
+
+typedef struct sgm_handle sgm_handle;
+
+/* ---- device / handle management ------------------------------------------------------ */
+/* Number of visible HIP devices (0 if none / runtime unavailable). Never throws.           */
+int  sgm_device_count(void);
+
+/* Create a matcher handle bound to `device` (reference ctor: abstractStereoMatcher.h:15,
+ * subclasses call init(), matcherOpenCVSGBM.h:10-14). Cheap: no device allocation happens
+ * until the first match (the reference constructs every matcher lazily on the first frame,
+ * generate_disparity.cpp:268-278). Returns SGM_ERR_DEVICE if `device` is not visible.     */
+int  sgm_create(sgm_handle** out, int device);
+void sgm_destroy(sgm_handle* h);
+
+/* Defaults: census mode = north-star config (P1 10, P2 120, uniq 5, subpixel+LR on);
+ * OCV modes = the generate_disparity node defaults (generate_disparity.cpp:100-112).      */
+void sgm_default_params(sgm_params* p, int mode);
+
+/* Store parameters. Like the reference's setters this never fails on values; invalid
+ * combinations surface at match time (matcherOpenCVSGBM.cpp:37-43 behaviour).            */
+int  sgm_set_params(sgm_handle* h, const sgm_params* p);
+int  sgm_get_params(const sgm_handle* h, sgm_params* p);
+
+/* Validate parameters for a W-wide image without matching (0 = would run).                */
+int  sgm_check_params(const sgm_params* p, int width, int height);
+
+/* ---- matching -------------------------------------------------------------------------- */
+/* Host buffers in, host buffer out; synchronous. L/R: W x H u8 mono (stride bytes);
+ * disp: W x H int16 (out_stride in elements). Replaces cv::StereoSGBM::compute
+ * (matcherOpenCVSGBM.cpp:21).                                                              */
+int  sgm_match(sgm_handle* h, const uint8_t* left, const uint8_t* right,
+               int width, int height, size_t stride,
+               int16_t* disp, size_t out_stride);
+
+/* Device buffers in/out (already resident in HBM), asynchronous on `stream` (hipStream_t,
+ * NULL = the handle's own stream). The handle's device must own the buffers.              */
+int  sgm_match_device(sgm_handle* h, const uint8_t* d_left, const uint8_t* d_right,
+                      int width, int height, size_t stride,
+                      int16_t* d_disp, size_t out_stride, void* stream);
+
+/* Frame batch, sharded frame i -> devices[i % n_dev] with one host thread + stream per
+ * device (SURVEY §8e "frame batch"). Host buffers; synchronous; no cross-device traffic.
+ * n_dev <= 0 or devices == NULL: all visible devices.                                      */
+int  sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights,
+                     int n_frames, int width, int height, size_t stride,
+                     int16_t* const* disps, size_t out_stride,
+                     const int* devices, int n_dev);
+
+/* Synchronise the handle's stream (after sgm_match_device with stream == NULL).          */
+int  sgm_synchronize(sgm_handle* h);
+
+const char* sgm_last_error(const sgm_handle* h);
+
+/* ---- profiling: per-stage device time (hipEvents on the handle's stream) ---------------- */
+#define SGM_MAX_STAGES 16
+/* enable != 0: (re)start recording a hipEvent before/after every stage of every match;
+ * the records of all matches since the last enable are kept (no host sync per match).     */
+int  sgm_set_profiling(sgm_handle* h, int enable);
+/* Synchronises on the last record, fills up to `max` per-stage AVERAGE times (ms) over the
+ * recorded matches of the current geometry; returns the number of stages.                */
+int  sgm_get_stage_times(sgm_handle* h, float* ms, int max);
+/* Number of matches averaged by sgm_get_stage_times.                                      */
+int  sgm_profiled_matches(const sgm_handle* h);
+const char* sgm_stage_name(const sgm_handle* h, int i);
+/* Algorithmic HBM bytes of stage i for the last match geometry. */
+double sgm_stage_bytes(const sgm_handle* h, int i);
+
+/* ---- stage entry points (parity tests compare each stage with the CPU oracle) ----------- */
+/* 9x7 census codes of one image (host buffers; out: W x H uint64, row-major).             */
+int  sgm_debug_census(sgm_handle* h, const uint8_t* img, int width, int height,
+                      size_t stride, uint64_t* out);
+/* Census mode: u8 path-cost volume of direction `dir` (0..6; see DESIGN.md for the order),
+ * layout [H][width1][D]. Runs census + that direction only.                               */
+int  sgm_debug_census_path(sgm_handle* h, const uint8_t* left, const uint8_t* right,
+                           int width, int height, size_t stride, int dir, uint8_t* vol);
+/* OCV modes: int16 aggregated matching cost C' = SAD + P2 used by the path recurrence,
+ * layout [H][width1][D].                                                                  */
+int  sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* left, const uint8_t* right,
+                        int width, int height, size_t stride, int16_t* cost);
+/* 3x3 median (replicate border) and speckle filter on a host int16 image, in place.       */
+int  sgm_debug_median3(sgm_handle* h, int16_t* disp, int width, int height);
+int  sgm_debug_speckle(sgm_handle* h, int16_t* disp, int width, int height,
+                       int new_val, int max_size, int max_diff);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGM_HIP_H */

@@ -1,0 +1,180 @@
+"""GPU parity — census-SGM (north-star mode). Every comparison is bit-exact (int16/u8/u64).
+
+Stage by stage against the CPU oracle: census codes, each of the 7 stored path volumes,
+then the full pipeline (dir 7 + 8-way sum + WTA + uniqueness + subpixel + LR), post
+filters, golden fixtures, and the BASELINE sizes (1920x1080 D=128 / D=256).
+"""
+import numpy as np
+import pytest
+
+from conftest import to_oracle_params
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (5, 7), (48, 64), (37, 101), (72, 300)])
+def test_census_codes(engine, oracle, shape):
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1])
+    img = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    img[::3, ::2] = 77
+    assert np.array_equal(engine.census(img), oracle.census(img))
+
+
+@pytest.mark.parametrize("D,minD", [(16, 0), (32, -7), (64, 3), (128, 0), (256, 0), (512, 0), (48, 2), (80, -3)])
+@pytest.mark.parametrize("dirn", range(7))
+def test_census_path_volumes(engine, oracle, synth, pkg, dirn, D, minD):
+    h = 23
+    w = max(D + minD, 0) + 57
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=D + dirn)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=minD, p1=9, p2=110)
+    engine.set_params(p)
+    got = engine.census_path(left, right, dirn)
+    ref = oracle.census_path(to_oracle_params(oracle, p), left, right, dirn)
+    assert np.array_equal(got, ref), f"dir {dirn}: {(got != ref).sum()} cells differ"
+
+
+CASES = [
+    dict(num_disparities=64),
+    dict(num_disparities=64, subpixel=0),
+    dict(num_disparities=64, lr_check=0),
+    dict(num_disparities=32, min_disparity=5, uniqueness_ratio=15),
+    dict(num_disparities=32, min_disparity=-9),
+    dict(num_disparities=16, p1=3, p2=20, disp12_max_diff=3),
+    dict(num_disparities=128, median=1),
+    dict(num_disparities=96, speckle_window_size=30, speckle_range=2, median=1),
+    dict(num_disparities=256, uniqueness_ratio=0),
+    dict(num_disparities=512),
+    dict(num_disparities=64, p2=250),         # clamped to 193 (u8 path costs)
+]
+
+
+@pytest.mark.parametrize("kw", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_census_pipeline(engine, oracle, synth, pkg, kw):
+    D, minD = kw["num_disparities"], kw.get("min_disparity", 0)
+    h, w = 61, max(D + minD, 0) + 133
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=D + 17)
+    p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+def test_census_edge_geometry(engine, oracle, pkg):
+    rng = np.random.default_rng(3)
+    for (h, w, D, minD) in [(4, 20, 16, 0), (3, 17, 16, 0), (9, 16, 16, 0), (30, 40, 48, 0), (2, 200, 64, -30)]:
+        left = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        right = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=minD, median=1)
+        engine.set_params(p)
+        assert np.array_equal(engine.match(left, right), oracle.match(to_oracle_params(oracle, p), left, right))
+
+
+def test_census_strided_host_buffers(engine, oracle, synth, pkg):
+    left, right, _ = synth.stereo_pair(40, 150, 0, 32, seed=4)
+    big_l = np.zeros((40, 160), np.uint8)
+    big_r = np.zeros((40, 160), np.uint8)
+    big_l[:, :150], big_r[:, :150] = left, right
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=32)
+    engine.set_params(p)
+    out = np.full((40, 170), 1234, np.int16)
+    import ctypes
+    rc = engine.lib.sgm_match(engine.h, ctypes.c_void_p(big_l.ctypes.data), ctypes.c_void_p(big_r.ctypes.data),
+                              150, 40, 160, ctypes.c_void_p(out.ctypes.data), 170)
+    assert rc == 0
+    assert np.array_equal(out[:, :150], oracle.match(to_oracle_params(oracle, p), left, right))
+    assert (out[:, 150:] == 1234).all()
+
+
+def test_bad_params_fail_at_match_time(engine, pkg):
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=40)
+    engine.set_params(p)                     # setters never fail (reference behaviour)
+    z = np.zeros((16, 64), np.uint8)
+    with pytest.raises(pkg.SGMError) as e:
+        engine.match(z, z)
+    assert e.value.code == pkg.SGM_ERR_PARAM and "16" in str(e.value)
+
+
+def test_golden_fixtures(engine, oracle, pkg):
+    import os
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    n = 0
+    for f in sorted(os.listdir(gdir)):
+        if not f.endswith(".npz"):
+            continue
+        z = np.load(os.path.join(gdir, f), allow_pickle=False)
+        p = pkg.SgmParams()
+        for k, v in zip(z["param_names"], z["param_values"]):
+            setattr(p, str(k), int(v))
+        engine.set_params(p)
+        got = engine.match(z["left"], z["right"])
+        assert np.array_equal(got, z["disp"]), f"{f}: {(got != z['disp']).sum()} pixels differ"
+        n += 1
+    assert n >= 8
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_full_size_baseline_configs(engine, oracle, synth, pkg, D):
+    """BASELINE configs C2 (D=128, no subpix/LR) and C3 (D=256 + subpix + LR) at 1920x1080,
+    bit-exact against the oracle (multi-threaded CPU, a few seconds on the box)."""
+    left, right, _ = synth.stereo_pair(1080, 1920, 0, D, seed=D)
+    kw = dict(num_disparities=D, p1=10, p2=120, uniqueness_ratio=5)
+    if D == 128:
+        kw.update(subpixel=0, lr_check=0)
+    p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    # size-independent sanity: accuracy vs the synthetic truth
+    _, _, g = synth.stereo_pair(1080, 1920, 0, D, seed=D)
+    m = got != -16
+    assert m.mean() > 0.6 and np.median(np.abs(got[m] / 16.0 - g[m])) < 0.6
+
+
+def test_repeat_and_resize(engine, oracle, synth, pkg):
+    """Workspace reuse across frames and geometry/parameter changes between frames."""
+    for (h, w, D) in [(40, 120, 32), (64, 200, 64), (40, 120, 32), (30, 90, 16)]:
+        left, right, _ = synth.stereo_pair(h, w, 0, D, seed=h + w)
+        p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D)
+        engine.set_params(p)
+        a = engine.match(left, right)
+        b = engine.match(left, right)
+        assert np.array_equal(a, b)
+        assert np.array_equal(a, oracle.match(to_oracle_params(oracle, p), left, right))
+
+
+def test_batch_equals_single(engine, pkg, synth):
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    frames = [synth.stereo_pair(48, 160, 0, 64, seed=100 + i) for i in range(5)]
+    outs = engine.match_batch([f[0] for f in frames], [f[1] for f in frames])
+    for (l, r, _), o in zip(frames, outs):
+        assert np.array_equal(o, engine.match(l, r))
+
+
+def test_device_pointer_path(engine, pkg, synth):
+    torch = pytest.importorskip("torch")
+    left, right, _ = synth.stereo_pair(64, 256, 0, 64, seed=9)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    ref = engine.match(left, right)
+    dl = torch.from_numpy(left).cuda()
+    dr = torch.from_numpy(right).cuda()
+    out = torch.empty((64, 256), dtype=torch.int16, device="cuda")
+    stream = torch.cuda.current_stream()
+    engine.match_device(dl.data_ptr(), dr.data_ptr(), 256, 64, 256, out.data_ptr(), 256, stream.cuda_stream)
+    stream.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_profiling_stage_times(engine, pkg, synth):
+    left, right, _ = synth.stereo_pair(64, 256, 0, 64, seed=9)
+    engine.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64))
+    engine.set_profiling(True)
+    engine.match(left, right)
+    st = engine.stage_times()
+    engine.set_profiling(False)
+    names = [s[0] for s in st]
+    assert names[:3] == ["census", "paths7", "final_wta_lr"]
+    assert all(t >= 0 for _, t, _ in st) and all(b > 0 for _, _, b in st)
