@@ -137,7 +137,9 @@ def main():
         dl.append(torch.from_numpy(l).to(device))
         dr.append(torch.from_numpy(r).to(device))
     out = torch.empty((args.frames, H, W), dtype=torch.int16, device=device)
-    stream = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    tstream = torch.cuda.Stream(device)        # the stream every kernel and HIP event runs on
+    stream = tstream.cuda_stream
 
     def step():
         for f in range(args.frames):

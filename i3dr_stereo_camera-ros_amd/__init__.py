@@ -74,6 +74,13 @@ def load_library(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"libsgm_hip.so not found at {path}: run build() / build_ext.py first")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7).
+    # Loading torch first makes the dynamic loader bind this library to that same copy, so
+    # device pointers and streams from torch are valid here (and torch still finds the GPU).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     P = ctypes.POINTER
     vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int

@@ -203,33 +203,38 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     }
 }
 
-// one wave per row: S = saturate(sum L) then the shared WTA + LR row code
+// one wave per row: S = saturate(sum L) then the shared batched WTA + row epilogue
 template <int DPL>
 __global__ __launch_bounds__(64) void k_ocv_wta(const int16_t* __restrict__ vols, size_t vol_elems, int ndir, Geom g,
                                                 int16_t* __restrict__ out, size_t out_stride)
 {
-    extern __shared__ int lds32[];
-    int* d2c = lds32;
-    int16_t* drow = (int16_t*)(lds32 + g.W);
-    int16_t* d2 = drow + g.W;
+    extern __shared__ uint32_t lds_ocv[];
+    RowLds R(lds_ocv, g.W);
     const int lane = threadIdx.x, y = blockIdx.x;
-    for (int x = lane; x < g.W; x += 64) { drow[x] = (int16_t)g.invalid; d2[x] = (int16_t)g.invalid; d2c[x] = kMaxCost; }
-    __syncthreads();
-    for (int x1 = g.width1 - 1; x1 >= 0; x1--) {
-        const size_t o = ((size_t)y * g.width1 + x1) * g.D;
-        int S[DPL];
+    R.init(g, lane);
+    for (int i0 = 0; i0 < g.width1; i0 += 4) {
+        int S[4][DPL], xs[4], nvalid = 0;
 #pragma unroll
-        for (int k = 0; k < DPL; k++) {
-            const int d = lane * DPL + k;
-            int s = 0;
-            if (d < g.D)
+        for (int u = 0; u < 4; u++) {
+            const int x1 = g.width1 - 1 - (i0 + u);
+            xs[u] = x1 + g.minX1;
+#pragma unroll
+            for (int k = 0; k < DPL; k++) S[u][k] = 1 << 20;
+            if (x1 < 0) continue;
+            nvalid = u + 1;
+            const size_t o = ((size_t)y * g.width1 + x1) * g.D;
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                const int d = lane * DPL + k;
+                if (d >= g.D) continue;
+                int s = 0;
                 for (int r = 0; r < ndir; r++) s += vols[(size_t)r * vol_elems + o + d];
-            S[k] = d < g.D ? min(max(s, -32768), kMaxCost) : (1 << 20);
+                S[u][k] = min(max(s, -32768), kMaxCost);
+            }
         }
-        wta_pixel<DPL>(S, lane, x1 + g.minX1, g, drow, d2, d2c);
+        wta_batch<DPL, 4>(S, lane, xs, nvalid, g, R.drow, R.bst, R.mins);
     }
-    __syncthreads();
-    lr_check_store(g, lane, drow, d2, out + (size_t)y * out_stride);
+    row_finish(g, lane, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
 // ------------------------------------------------------------------------------------
@@ -269,7 +274,7 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
 hipError_t launch_ocv_wta(const int16_t* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
                           size_t out_stride, hipStream_t st)
 {
-    const size_t lds = (size_t)8 * g.W;
+    const size_t lds = RowLds::bytes(g.W);
     switch (dpl_for(g.D)) {
     case 1: hipLaunchKernelGGL(k_ocv_wta<1>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
     case 2: hipLaunchKernelGGL(k_ocv_wta<2>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;

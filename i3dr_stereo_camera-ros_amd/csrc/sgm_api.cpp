@@ -38,6 +38,7 @@ using sgm::Geom;
 namespace {
 
 constexpr size_t kAlign = 256;
+constexpr size_t kTrashBytes = 4096;   // >= 64 lanes x 8 disparities (census_sgm.hip)
 inline size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 // effective parameters — identical rules to the oracle (oracle/sgm_oracle.c effective())
@@ -196,7 +197,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
     if (p.mode == SGM_MODE_CENSUS8) {
         l.cL = take(WH * 8);
         l.cR = take(WH * 8);
-        l.vol_bytes = align_up(cells);
+        l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
         l.vols = take(l.vol_bytes * 7);
     } else {
         l.planes = take(WH * 4);

@@ -80,49 +80,118 @@ __device__ __forceinline__ int pick(const int (&S)[DPL], int k) {
     return r;
 }
 
-// Winner-take-all for the pixel at image column x (x descending over a row), OpenCV
-// computeDisparitySGBM semantics: first minimal S, uniqueness
-// reject (no disp2 update), disp2 "strictly better" update, parabolic subpixel with C
-// truncating division. S[k] for d = lane*DPL + k; lanes/entries with d >= D hold a value
-// larger than any real S. Writes drow[x] / d2 / d2c (LDS) from lane 0.
-template <int DPL>
-__device__ __forceinline__ void wta_pixel(const int (&S)[DPL], int lane, int x, const Geom& g,
-                                          int16_t* drow, int16_t* d2, int* d2c)
-{
-    int lminS = S[0], lk = 0;
-#pragma unroll
-    for (int k = 1; k < DPL; k++)
-        if (S[k] < lminS) { lminS = S[k]; lk = k; }
-    const int minS = wave_min(lminS);
-    const unsigned long long mm = __ballot(lminS == minS);
-    const int bl = __builtin_ctzll(mm);
-    const int best = bl * DPL + __builtin_amdgcn_readlane(lk, bl);
-    bool rej = false;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) {
-        const int d = lane * DPL + k;
-        rej |= (d < g.D) && (S[k] * (100 - g.uniq) < minS * 100) && (abs(d - best) > 1);
-    }
-    if (__ballot(rej) != 0ull) return;
-    int d16 = best * 16;
-    if (g.subpix && best > 0 && best < g.D - 1) {
-        const int sm = __builtin_amdgcn_readlane(pick<DPL>(S, (best - 1) % DPL), (best - 1) / DPL);
-        const int sp = __builtin_amdgcn_readlane(pick<DPL>(S, (best + 1) % DPL), (best + 1) / DPL);
-        const int den = max(sm + sp - 2 * minS, 1);
-        d16 += tdiv((sm - sp) * 16 + den, 2 * den);
-    }
-    if (lane == 0) {
-        const int x2 = x - best - g.minD;
-        if (d2c[x2] > minS) { d2c[x2] = minS; d2[x2] = (int16_t)(best + g.minD); }
-        drow[x] = (int16_t)(d16 + g.minD * 16);
-    }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
 }
 
-// Row epilogue: LR check (OpenCV: both rounded candidates inconsistent -> invalid) and
-// store of the full row (columns outside [minX1, maxX1) stay invalid).
-__device__ __forceinline__ void lr_check_store(const Geom& g, int lane, const int16_t* drow, const int16_t* d2,
-                                               int16_t* orow)
+// Winner-take-all of U pixels at once (OpenCV computeDisparitySGBM semantics, SURVEY
+// Appendix A.6), branch-free so the U independent reduction chains interleave:
+//   best  = first d with the minimal S;
+//   reject if some d with |d - best| > 1 has S[d]*(100-uniq) < minS*100;
+//   subpixel d16 = 16*best + ((S[best-1]-S[best+1])*16 + den) / (2*den), C truncation,
+//   den = max(S[best-1] + S[best+1] - 2*S[best], 1), only for 0 < best < D-1.
+// S[u][k] holds d = lane*DPL + k; entries with d >= D must be larger than any real S.
+// Results for pixel u (columns xs[u], u < nvalid) go to LDS from lane 0:
+//   drow[x] = d16 + 16*minD (left untouched when rejected), bst[x] = best (-1 if rejected),
+//   mins[x] = minS. disp2 is derived later from (bst, mins) by row_finish().
+template <int DPL, int U>
+__device__ __forceinline__ void wta_batch(const int (&S)[U][DPL], int lane, const int (&xs)[U], int nvalid,
+                                          const Geom& g, int16_t* drow, int16_t* bst, uint16_t* mins)
 {
+    int lmin[U], lk[U], minS[U], best[U], d16[U];
+    bool rej[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        lmin[u] = S[u][0]; lk[u] = 0;
+#pragma unroll
+        for (int k = 1; k < DPL; k++) {
+            const bool lt = S[u][k] < lmin[u];
+            lmin[u] = lt ? S[u][k] : lmin[u];
+            lk[u] = lt ? k : lk[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) minS[u] = wave_min(lmin[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int bl = __builtin_ctzll(__ballot(lmin[u] == minS[u]));
+        best[u] = bl * DPL + __builtin_amdgcn_readlane(lk[u], bl);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        bool r = false;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = lane * DPL + k;
+            r |= (d < g.D) && (S[u][k] * (100 - g.uniq) < minS[u] * 100) && (abs(d - best[u]) > 1);
+        }
+        rej[u] = __ballot(r) != 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        // S[best-1], S[best+1]: masked per-lane contribution + readlane (no dynamic
+        // register indexing, which hipcc would lower to scratch)
+        const int bm = max(best[u] - 1, 0), bp = min(best[u] + 1, g.D - 1);
+        int vm = 0, vp = 0;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = lane * DPL + k;
+            vm += d == bm ? S[u][k] : 0;
+            vp += d == bp ? S[u][k] : 0;
+        }
+        const int sm = __builtin_amdgcn_readlane(vm, bm / DPL);
+        const int sp = __builtin_amdgcn_readlane(vp, bp / DPL);
+        const int den = max(sm + sp - 2 * minS[u], 1);
+        const bool use = g.subpix && best[u] > 0 && best[u] < g.D - 1;
+        d16[u] = best[u] * 16 + (use ? tdiv((sm - sp) * 16 + den, 2 * den) : 0);
+    }
+    // lane u stores pixel u; every other lane (and pixels u >= nvalid) hits its own dummy
+    // slot at index W + lane, so the LDS stores need no exec-masked branch.
+    int x = g.W + lane, b = -1, m = 32767, dv = 0, keep = 1;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const bool me = lane == u && u < nvalid;
+        x = me ? xs[u] : x;
+        b = me ? (rej[u] ? -1 : best[u]) : b;
+        m = me ? minS[u] : m;
+        dv = me ? d16[u] + g.minD * 16 : dv;
+        keep = me ? (rej[u] ? 1 : 0) : keep;
+    }
+    bst[x] = (int16_t)b;
+    mins[x] = (uint16_t)m;
+    drow[keep ? g.W + lane : x] = (int16_t)dv;   // rejected pixels keep the invalid value
+}
+
+// Row epilogue, after every pixel of the row went through wta_batch:
+//  1. disp2 (right-view disparity, OpenCV's x-descending "strictly better" rule): for each
+//     target column x2 the pixel with the smallest minS wins, ties -> the largest x. This
+//     is an LDS atomicMin over key = minS << 16 | (0xFFFF - x). disp2 starts at the SCALED
+//     invalid value (OpenCV quirk: it can look valid when minD > 0), and minS = 32767
+//     never updates (disp2cost starts at MAX_COST).
+//  2. LR check: invalid iff both rounded candidates are in range, have disp2 >= minD and
+//     differ by more than disp12.
+//  3. store of the full row (columns outside [minX1, maxX1) stay invalid).
+// `key` needs W uint32; `d2` may alias `mins` (mins is dead after step 1).
+__device__ __forceinline__ void row_finish(const Geom& g, int lane, const int16_t* drow, const int16_t* bst,
+                                           const uint16_t* mins, uint32_t* key, int16_t* d2, int16_t* orow)
+{
+    __syncthreads();
+    for (int x = g.minX1 + lane; x < g.maxX1; x += 64) {
+        const int b = bst[x];
+        const int m = mins[x];
+        if (b >= 0 && m < 32767) {
+            const int x2 = x - b - g.minD;
+            atomicMin(&key[x2], ((uint32_t)m << 16) | (uint32_t)(0xFFFF - x));
+        }
+    }
+    __syncthreads();
+    for (int x2 = lane; x2 < g.W; x2 += 64) {
+        const uint32_t k = key[x2];
+        d2[x2] = (int16_t)(k == 0xFFFFFFFFu ? g.invalid : bst[0xFFFF - (int)(k & 0xFFFF)] + g.minD);
+    }
+    __syncthreads();
     for (int x = lane; x < g.W; x += 64) {
         int d1 = drow[x];
         if (g.lr && d1 != g.invalid) {
@@ -135,6 +204,25 @@ __device__ __forceinline__ void lr_check_store(const Geom& g, int lane, const in
         orow[x] = (int16_t)d1;
     }
 }
+
+// LDS carve-up of the per-row WTA state: key u32 [W] | drow i16 | bst i16 | mins u16, the
+// last three with 64 extra dummy slots (index W + lane) for branch-free stores.
+struct RowLds {
+    uint32_t* key; int16_t* drow; int16_t* bst; uint16_t* mins;
+    static size_t bytes(int W) { return (size_t)4 * W + (size_t)6 * (W + 64) + 16; }
+    __device__ RowLds(void* base, int W) {
+        key = (uint32_t*)base;
+        drow = (int16_t*)(key + W);
+        bst = drow + W + 64;
+        mins = (uint16_t*)(bst + W + 64);
+    }
+    __device__ void init(const Geom& g, int lane) {
+        for (int x = lane; x < g.W; x += 64) {
+            key[x] = 0xFFFFFFFFu; drow[x] = (int16_t)g.invalid; bst[x] = -1; mins[x] = 32767;
+        }
+        __syncthreads();
+    }
+};
 
 // Pack DPL u8 path costs of one lane into the per-lane store word.
 template <int DPL> struct LaneVec;

@@ -162,7 +162,8 @@ def test_device_pointer_path(engine, pkg, synth):
     dl = torch.from_numpy(left).cuda()
     dr = torch.from_numpy(right).cuda()
     out = torch.empty((64, 256), dtype=torch.int16, device="cuda")
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()                 # explicit non-default stream handed to the C-ABI
+    stream.wait_stream(torch.cuda.current_stream())
     engine.match_device(dl.data_ptr(), dr.data_ptr(), 256, 64, 256, out.data_ptr(), 256, stream.cuda_stream)
     stream.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref)
