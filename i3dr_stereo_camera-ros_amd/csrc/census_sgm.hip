@@ -2,12 +2,13 @@
 //
 // Spec: SURVEY.md Appendix B (build-defined; CPU definition oracle/sgm_oracle.c
 // `census_step`/`census_path`/`wta_pixel`). Pipeline per frame:
-//   k_census9x7      L,R u8            -> census codes u64 (2 x W x H)
-//   k_census_paths   codes             -> 7 u8 path volumes [H][width1][D] (dirs 0..6)
-//   k_census_final   codes + 7 volumes -> dir 7 (r = (-1,0)) fused with the 8-way sum,
-//                                         WTA, uniqueness, subpixel, disp2 and LR check
+//   k_census9x7       L,R u8        -> census codes u64 (2 x W x H)
+//   k_census_paths16  codes         -> 8 u8 path volumes [H][width1][D], all directions in
+//                                      one launch (6 row sweeps + 2 horizontal scans)
+//   k_census_wta      8 volumes     -> S = sum of the 8 paths, WTA, uniqueness, subpixel,
+//                                      disp2 and LR check (one workgroup per row)
 // The matching cost popcount(cL ^ cR) is recomputed on the fly in every path (never
-// stored); S = sum of the 8 paths never touches HBM.
+// stored); S never touches HBM.
 #include "sgm_device.h"
 
 namespace sgm {
@@ -48,323 +49,355 @@ __global__ __launch_bounds__(256) void k_census9x7(const uint8_t* __restrict__ L
     out[(size_t)y * W + x] = code;
 }
 
-// ------------------------------------------------------------------------------------
-// Path recurrence of one cell for the DPL disparities of this lane.
-//   L(d) = C(d) + min(Lp(d), Lp(d-1)+P1, Lp(d+1)+P1, minLp+P2) - minLp
-// Lanes with d >= D hold kInf. `cost[k]` = popcount(cL ^ cR(x - minD - d)).
-// ------------------------------------------------------------------------------------
+// ====================================================================================
+// P16 path engine. A path line owns one 16-lane row of a wave: lane p holds disparities
+// d = p*DPL .. p*DPL + DPL-1 (DPL = D_pad/16, D_pad = 16*DPL >= D), two per 32-bit
+// register as packed u16 (v_pk_*_u16). The recurrence is kept in relative form
+//     L(d)  = C(d) + min(L'(d), min(L'(d-1), L'(d+1)) + P1, P2),   L' = Lprev - min Lprev
+// which equals SGM's C + min(Lp, Lp+-1 + P1, minLp + P2) - minLp exactly (all values
+// <= 255 because C <= 62 and P2 <= 193). min over D is a 4-step DPP reduction inside the
+// row; the d-1 / d+1 neighbours are v_alignbit of adjacent registers plus one row_shr /
+// row_shl DPP for the lane boundary. Entries with d >= D are forced to 0xFFFF.
+//
+// Memory-op discipline: gfx950 counts loads and stores on one in-order vmcnt and hipcc
+// only emits counted waits when every path through a loop body issues the same VMEM ops.
+// So loops issue a fixed sequence: clamped prefetches, and cells that must not be written
+// (outside the image, d >= D, padding steps) go to a per-volume trash slot.
+// ====================================================================================
 template <int DPL>
-__device__ __forceinline__ int path_step(const int (&cost)[DPL], const int (&Lp)[DPL], int mLp, bool pv,
-                                         int lane, int D, int P1, int P2, int (&Lout)[DPL])
+__device__ __forceinline__ void store_pairs(uint8_t* dst, const uint32_t (&L)[DPL / 2])
 {
-    const int fromLeft = dpp_shr1(Lp[DPL - 1], kInf);   // Lp(d-1) for k = 0
-    const int fromRight = dpp_shl1(Lp[0], kInf);        // Lp(d+1) for k = DPL-1
-    const int q = mLp + P2;
-    int lmin = kInf;
+    // (lo, hi) u16 pairs with values <= 255 -> DPL consecutive bytes
+    if constexpr (DPL == 2) {
+        *(uint16_t*)dst = (uint16_t)__builtin_amdgcn_perm(0u, L[0], 0x0c0c0200u);
+    } else if constexpr (DPL == 4) {
+        *(uint32_t*)dst = __builtin_amdgcn_perm(L[1], L[0], 0x06040200u);
+    } else if constexpr (DPL == 8) {
+        *(uint2*)dst = make_uint2(__builtin_amdgcn_perm(L[1], L[0], 0x06040200u),
+                                  __builtin_amdgcn_perm(L[3], L[2], 0x06040200u));
+    } else {
 #pragma unroll
-    for (int k = 0; k < DPL; k++) {
-        const int lm1 = k > 0 ? Lp[k - 1] : fromLeft;
-        const int lp1 = k < DPL - 1 ? Lp[k + 1] : fromRight;
-        int t = min(lm1, lp1) + P1;
-        t = min(min(Lp[k], t), q);
-        int v = pv ? cost[k] + t - mLp : cost[k];
-        v = (lane * DPL + k) < D ? v : kInf;
-        Lout[k] = v;
-        lmin = min(lmin, v);
-    }
-    return lmin;
-}
-
-struct PathLaunch {
-    int blk_start[8];   // first block of dir i (dirs 0..6), blk_start[7] = total
-    int xb_lo[6];       // first line base column of row-sweep dir i
-};
-
-constexpr int kG = 4;       // adjacent lines (columns) per wave in the row sweeps
-constexpr int kChunk = 16;  // steps per unrolled chunk of the horizontal scans
-
-// Memory-op discipline (why the loops look the way they do): gfx950 counts loads AND
-// stores on one in-order vmcnt. hipcc only emits counted waits (vmcnt(N)) when every path
-// through the loop body issues the same VMEM ops in the same order; a conditional store
-// or prefetch makes it fall back to vmcnt(0), i.e. one full memory round trip per step.
-// So every loop body below issues an unconditional, fixed sequence: prefetches use clamped
-// indices, and cells that must not be written (outside the image, lanes with d >= D,
-// padding steps) store into a per-volume trash slot instead of branching around the store.
-
-// Per-step inputs of a row sweep: the lane's window of right codes (DPL + kG - 1 values
-// cover its DPL disparities for the kG adjacent columns) and the kG left codes (scalar).
-template <int DPL>
-struct RowIn {
-    uint64_t cr[DPL + kG - 1];
-    uint64_t cl[kG];
-};
-
-template <int DPL>
-__device__ __forceinline__ void row_load(RowIn<DPL>& in, const uint64_t* __restrict__ cL,
-                                         const uint64_t* __restrict__ cR, const Geom& g, int rx, int ry, int xb,
-                                         int s, int lane)
-{
-    const int y = ry > 0 ? s : g.H - 1 - s;
-    const uint64_t* cLr = cL + (size_t)y * g.W;
-    const uint64_t* cRr = cR + (size_t)y * g.W;
-    const int xs = xb + rx * s;
-    const int jb = xs - g.minD - lane * DPL - (DPL - 1);
-#pragma unroll
-    for (int m = 0; m < DPL + kG - 1; m++) in.cr[m] = cRr[min(max(jb + m, 0), g.W - 1)];
-#pragma unroll
-    for (int j = 0; j < kG; j++) in.cl[j] = cLr[min(max(xs + j, 0), g.W - 1)];
-}
-
-template <int DPL>
-struct RowState {
-    int Lp[kG][DPL];
-    int mLp[kG];
-    bool pv[kG];
-};
-
-template <int DPL>
-__device__ __forceinline__ void row_step(const RowIn<DPL>& in, RowState<DPL>& st, uint8_t* __restrict__ V,
-                                         uint8_t* __restrict__ trash, const Geom& g, int rx, int ry, int xb, int s,
-                                         int s1, int lane)
-{
-    using VT = typename LaneVec<DPL>::T;
-    const int y = ry > 0 ? s : g.H - 1 - s;
-    const int xs = xb + rx * s;
-    const bool active = lane * DPL < g.D;
-#pragma unroll
-    for (int j = 0; j < kG; j++) {
-        const int x = xs + j;
-        const bool valid = s < s1 && x >= g.minX1 && x < g.maxX1;        // wave-uniform
-        int cost[DPL], L[DPL];
-#pragma unroll
-        for (int k = 0; k < DPL; k++) cost[k] = popc64(in.cl[j] ^ in.cr[j - k + DPL - 1]);
-        const int lmin = path_step<DPL>(cost, st.Lp[j], st.mLp[j], st.pv[j], lane, g.D, g.P1, g.P2, L);
-        uint8_t* dst = (valid && active) ? V + ((size_t)y * g.width1 + (x - g.minX1)) * g.D + lane * DPL
-                                         : trash + lane * DPL;
-        *(VT*)dst = pack_u8<DPL>(L);
-        st.mLp[j] = wave_min(lmin);
-#pragma unroll
-        for (int k = 0; k < DPL; k++) st.Lp[j][k] = L[k];
-        st.pv[j] = valid;
+        for (int q = 0; q < DPL / 16; q++)
+            ((uint4*)dst)[q] = make_uint4(__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
+                                          __builtin_amdgcn_perm(L[8 * q + 3], L[8 * q + 2], 0x06040200u),
+                                          __builtin_amdgcn_perm(L[8 * q + 5], L[8 * q + 4], 0x06040200u),
+                                          __builtin_amdgcn_perm(L[8 * q + 7], L[8 * q + 6], 0x06040200u));
     }
 }
 
-// Row sweep (dirs 0..5, ry != 0): the wave owns kG adjacent lines; line j at step s sits
-// at column xb + j + rx*s of row y(s). All D of each cell live in the wave. The inputs of
-// step s+1 are loaded (ping-pong registers) while step s computes.
-template <int DPL>
-__device__ __forceinline__ void row_sweep(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
-                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
-                                          int dir, int xb)
+// Hamming costs of the lane's DPL disparities as u16 pairs; crk(k) = right code of d = p*DPL + k
+template <int DPL, typename F>
+__device__ __forceinline__ void pair_costs(uint64_t cl, F crk, uint32_t (&C)[DPL / 2])
 {
-    const int lane = threadIdx.x;
-    const int rx = dir_rx(dir), ry = dir_ry(dir);
-    int s0, s1;
-    if (rx == 0) { s0 = 0; s1 = g.H; }
-    else if (rx > 0) { s0 = max(0, g.minX1 - xb - (kG - 1)); s1 = min(g.H, g.maxX1 - xb); }
-    else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + kG - g.minX1); }
-    if (s0 >= s1) return;
-    RowState<DPL> st;
 #pragma unroll
-    for (int j = 0; j < kG; j++) {
-        st.pv[j] = false;
-        st.mLp[j] = 0;
+    for (int i = 0; i < DPL / 2; i++)
+        C[i] = (uint32_t)popc64(cl ^ crk(2 * i)) | ((uint32_t)popc64(cl ^ crk(2 * i + 1)) << 16);
+}
+
+// One recurrence step of the lane's pairs. Lr: relative state in/out. Labs: absolute L.
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], const uint32_t (&C)[DPL / 2], uint32_t P1P1,
+                                         uint32_t P2P2, const uint32_t (&imask)[DPL / 2], uint32_t (&Labs)[DPL / 2])
+{
+    constexpr int M = DPL / 2;
+    const uint32_t X = row_shr1(Lr[M - 1], 0xFFFFFFFFu);   // previous lane: its .hi is L(d0 - 1)
+    const uint32_t Y = row_shl1(Lr[0], 0xFFFFFFFFu);       // next lane: its .lo is L(d0 + DPL)
+    uint32_t mn = 0xFFFFFFFFu;
+    uint32_t Oprev = alignbit16(Lr[0], X);                  // (L(d-1), L(d)) for pair 0
 #pragma unroll
-        for (int k = 0; k < DPL; k++) st.Lp[j][k] = kInf;
+    for (int i = 0; i < M; i++) {
+        const uint32_t Onext = (i + 1 < M) ? alignbit16(Lr[i + 1], Lr[i]) : alignbit16(Y, Lr[M - 1]);
+        const uint32_t u = pk_adds(pk_min(Oprev, Onext), P1P1);
+        const uint32_t v = pk_min(pk_min(u, Lr[i]), P2P2);
+        uint32_t L = pk_add(v, C[i]);
+        if (!EXACT) L |= imask[i];
+        Labs[i] = L;
+        mn = pk_min(mn, L);
+        Oprev = Onext;
     }
-    RowIn<DPL> A, B;
-    row_load<DPL>(A, cL, cR, g, rx, ry, xb, s0, lane);
-    for (int s = s0; s < s1; s += 2) {
-        row_load<DPL>(B, cL, cR, g, rx, ry, xb, min(s + 1, s1 - 1), lane);
-        row_step<DPL>(A, st, V, trash, g, rx, ry, xb, s, s1, lane);
-        row_load<DPL>(A, cL, cR, g, rx, ry, xb, min(s + 2, s1 - 1), lane);
-        row_step<DPL>(B, st, V, trash, g, rx, ry, xb, s + 1, s1, lane);
+    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
+#pragma unroll
+    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], mn);
+}
+
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL / 2])
+{
+#pragma unroll
+    for (int i = 0; i < DPL / 2; i++) {
+        const int d = p * DPL + 2 * i;
+        imask[i] = EXACT ? 0u : ((d < D ? 0u : 0xFFFFu) | (d + 1 < D ? 0u : 0xFFFF0000u));
     }
 }
 
-// Scalar operands of a horizontal scan, kChunk steps per vector load: lane j (< kChunk)
-// holds the left code and the window-entry right code of step (kChunk*chunk + j); step i
-// reads them with readlane, so no scalar-load latency sits on the recurrence chain.
-struct HChunk {
-    uint64_t cl, inc;
+struct PathLaunch16 {
+    int blk_start[9];    // workgroups of launch slot i (order kSlotDir), blk_start[8] = total
+    int xb_lo[8];        // row sweeps: first base column of the direction
+};
+// launch order: the two horizontal scans first (longest dependency chains), then rows
+__host__ __device__ constexpr int slot_dir(int i) { return i < 2 ? 6 + i : i - 2; }
+
+constexpr int kWG = 256;          // 4 waves
+constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
+constexpr int kColsPerWG = 16;    // row sweeps: 4 columns per wave
+
+// ---------------------------------------------------------------- horizontal scans ----
+// Scalar operands per step come from 16-step chunks held one value per lane (lane j of a
+// row holds step j) and are broadcast inside the row with ds_swizzle. The right-code
+// window slides by one column per step through a rotating register file (no moves).
+struct HChunk16 {
+    uint64_t cl, inj;
 };
 
-__device__ __forceinline__ HChunk hchunk_load(const uint64_t* cLr, const uint64_t* cRr, const Geom& g, int dirx,
-                                              int chunk, int lane, int DPLx64)
+template <int DPL, int DX>
+__device__ __forceinline__ HChunk16 hload16(const uint64_t* cLr, const uint64_t* cRr, const Geom& g, int chunk,
+                                            int p)
 {
-    const int i = chunk * kChunk + (lane & (kChunk - 1));
-    HChunk c;
-    if (dirx > 0) {   // x ascending from minX1; inc = code entering for step i + 1
-        const int x = g.minX1 + i;
-        c.cl = cLr[min(x, g.W - 1)];
-        c.inc = cRr[min(max(x + 1 - g.minD, 0), g.W - 1)];
-    } else {          // x descending from maxX1 - 1
-        const int x = g.maxX1 - 1 - i;
-        c.cl = cLr[min(max(x, 0), g.W - 1)];
-        c.inc = cRr[min(max(x - g.minD - DPLx64, 0), g.W - 1)];
-    }
+    const int i = chunk * 16 + p;
+    const int x = DX > 0 ? g.minX1 + i : g.maxX1 - 1 - i;
+    HChunk16 c;
+    c.cl = cLr[min(max(x, 0), g.W - 1)];
+    const int xr = DX > 0 ? x + 1 - g.minD : x - g.minD - 16 * DPL;   // code entering the window
+    c.inj = cRr[min(max(xr, 0), g.W - 1)];
     return c;
 }
 
-// Horizontal sweep, dir 6 (r = (1,0)): one wave per row, x ascending. The right-code
-// window slides by one column per step: lane l takes lane l-1's oldest code (DPP),
-// lane 0 takes cR(x + 1 - minD).
-template <int DPL>
-__device__ __forceinline__ void horiz_sweep(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
-                                            uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
-                                            int y)
+template <int DPL, bool EXACT, int DX>
+__device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
+                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
+                                          int y0)
 {
-    using VT = typename LaneVec<DPL>::T;
-    const int lane = threadIdx.x;
-    const bool active = lane * DPL < g.D;
-    const uint64_t* cLr = cL + (size_t)y * g.W;
-    const uint64_t* cRr = cR + (size_t)y * g.W;
-    uint64_t cr[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; k++) cr[k] = cRr[max(g.minX1 - g.minD - lane * DPL - k, 0)];
-    int Lp[DPL];
-#pragma unroll
-    for (int k = 0; k < DPL; k++) Lp[k] = kInf;
-    int mLp = 0;
-    bool pv = false;
-    uint8_t* row = V + (size_t)y * g.width1 * g.D + lane * DPL;
-    uint8_t* tr = trash + lane * DPL;
+    constexpr int M = DPL / 2;
+    constexpr int U = DPL > 16 ? DPL : 16;       // unroll: window rotation period and chunk size
+    const int lane = threadIdx.x & 63;
+    const int r = lane >> 4, p = lane & 15;
+    const int y = y0 + r;
+    const bool rowok = y < g.H;
+    const int yc = min(y, g.H - 1);
+    const uint64_t* cLr = cL + (size_t)yc * g.W;
+    const uint64_t* cRr = cR + (size_t)yc * g.W;
+    uint32_t imask[M];
+    make_imask<DPL, EXACT>(p, g.D, imask);
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = (uint32_t)g.P2 * 0x10001u;
     const int n = g.width1;
-    HChunk cur = hchunk_load(cLr, cRr, g, 1, 0, lane, 64 * DPL);
-    for (int c = 0; c * kChunk < n; c++) {
-        const HChunk nxt = hchunk_load(cLr, cRr, g, 1, c + 1, lane, 64 * DPL);
+    const int xfirst = DX > 0 ? g.minX1 : g.maxX1 - 1;
+    uint64_t cr[DPL];                             // physical window registers
 #pragma unroll
-        for (int j = 0; j < kChunk; j++) {
-            const int i = c * kChunk + j;
-            const uint64_t cl = readlane64(cur.cl, j);
-            const uint64_t inc = readlane64(cur.inc, j);
-            int cost[DPL], L[DPL];
+    for (int k = 0; k < DPL; k++) cr[k] = cRr[min(max(xfirst - g.minD - p * DPL - k, 0), g.W - 1)];
+    uint32_t Lr[M];
 #pragma unroll
-            for (int k = 0; k < DPL; k++) cost[k] = popc64(cl ^ cr[k]);
-            const int lmin = path_step<DPL>(cost, Lp, mLp, pv, lane, g.D, g.P1, g.P2, L);
-            *(VT*)((active && i < n) ? row + (size_t)i * g.D : tr) = pack_u8<DPL>(L);
-            mLp = wave_min(lmin);
+    for (int i = 0; i < M; i++) Lr[i] = imask[i];
+    uint8_t* rowbase = V + (size_t)yc * g.width1 * g.D + p * DPL;
+    uint8_t* tr = trash + lane * DPL;
+    const bool lane_ok = rowok && (EXACT || p * DPL < g.D);
+    HChunk16 cur = hload16<DPL, DX>(cLr, cRr, g, 0, p);
+    HChunk16 nxt = cur;
+    for (int b = 0; b * U < n; b++) {
+        static_for<0, U>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            if constexpr (t % 16 == 0) nxt = hload16<DPL, DX>(cLr, cRr, g, (b * U + t) / 16 + 1, p);
+            const int i = b * U + t;
+            const uint64_t cl = row_bcast_u64<t % 16>(cur.cl);
+            const uint64_t inj = row_bcast_u64<t % 16>(cur.inj);
+            // logical window index k lives in physical register (k - t) (DX>0) / (k + t) (DX<0)
+            uint32_t C[M], Labs[M];
+            pair_costs<DPL>(cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; }, C);
+            p16_step<DPL, EXACT>(Lr, C, P1P1, P2P2, imask, Labs);
+            const int x1 = DX > 0 ? i : n - 1 - i;
+            store_pairs<DPL>((lane_ok && i < n) ? rowbase + (size_t)x1 * g.D : tr, Labs);
+            if constexpr (DX > 0) {
+                constexpr int ph = ((DPL - 1 - t) % DPL + DPL) % DPL;
+                cr[ph] = row_shr1_u64(cr[ph], inj);
+            } else {
+                constexpr int ph = t % DPL;
+                cr[ph] = row_shl1_u64(cr[ph], inj);
+            }
+            if constexpr (t % 16 == 15) cur = nxt;
+        });
+    }
+}
+
+// ---------------------------------------------------------------- row sweeps ----------
+// Workgroup = 4 waves = 16 adjacent lines; slot j = 4*wave + row. Each step the WG stages
+// the row's right-code segment (16*DPL + 15 codes) and the 16 left codes in LDS, double-
+// buffered, one barrier per step; the segment is padded by one code per 16 so the lanes'
+// strided window reads spread over the banks.
+template <int DPL>
+struct RowSeg {
+    static constexpr int NSEG = 16 * DPL + 15;
+    static constexpr int NPAD = NSEG + NSEG / 16 + 1;        // padded cR part
+    static constexpr int NTOT = NSEG + 16;                   // codes staged per step
+    static constexpr int NLOAD = (NTOT + kWG - 1) / kWG;     // per thread
+    static constexpr int BUF = NPAD + 16 + kWG;              // + cL + dummy slots
+    static __device__ __forceinline__ int phys(int e) { return e + (e >> 4); }
+};
+
+template <int DPL>
+__device__ __forceinline__ void seg_load(uint64_t (&v)[RowSeg<DPL>::NLOAD], const uint64_t* cL, const uint64_t* cR,
+                                         const Geom& g, int rx, int ry, int xb, int s, int tid)
+{
+    using RS = RowSeg<DPL>;
+    const int y = ry > 0 ? s : g.H - 1 - s;
+    const int yc = min(max(y, 0), g.H - 1);
+    const uint64_t* cLr = cL + (size_t)yc * g.W;
+    const uint64_t* cRr = cR + (size_t)yc * g.W;
+    const int xs = xb + rx * s;
+    const int seg0 = xs - g.minD - 16 * DPL + 1;
 #pragma unroll
-            for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-            pv = true;
-            const uint64_t nw = dpp_shr1_u64(cr[DPL - 1], inc);
-#pragma unroll
-            for (int k = DPL - 1; k > 0; k--) cr[k] = cr[k - 1];
-            cr[0] = nw;
-        }
-        cur = nxt;
+    for (int m = 0; m < RS::NLOAD; m++) {
+        const int q = min(tid + m * kWG, RS::NTOT - 1);
+        const int idx = q < RS::NSEG ? seg0 + q : xs + (q - RS::NSEG);
+        v[m] = (q < RS::NSEG ? cRr : cLr)[min(max(idx, 0), g.W - 1)];
     }
 }
 
 template <int DPL>
-__global__ __launch_bounds__(64) void k_census_paths(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
-                                                     uint8_t* __restrict__ vols, size_t vol_bytes, size_t trash_off,
-                                                     Geom g, PathLaunch pl)
+__device__ __forceinline__ void seg_store(uint64_t* buf, const uint64_t (&v)[RowSeg<DPL>::NLOAD], int tid)
 {
-    const int b = blockIdx.x;
-    int dir = 0;
+    using RS = RowSeg<DPL>;
 #pragma unroll
-    for (int i = 1; i < 7; i++) dir += b >= pl.blk_start[i] ? 1 : 0;
-    const int lb = b - pl.blk_start[dir];
-    uint8_t* V = vols + (size_t)dir * vol_bytes;
-    uint8_t* trash = V + trash_off;
-    if (dir < 6) row_sweep<DPL>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kG);
-    else horiz_sweep<DPL>(cL, cR, V, trash, g, lb);
+    for (int m = 0; m < RS::NLOAD; m++) {
+        const int q0 = tid + m * kWG;
+        const int at = q0 < RS::NSEG ? RS::phys(q0) : (q0 < RS::NTOT ? RS::NPAD + (q0 - RS::NSEG) : RS::NPAD + 16 + tid);
+        buf[at] = v[m];
+    }
 }
 
-// ------------------------------------------------------------------------------------
-// Final pass: dir 7 (r = (-1,0), x descending) + S = L7 + sum of the 7 stored volumes,
-// WTA of kU pixels at a time (branch-free, wta_batch), then the row epilogue (disp2 via
-// LDS atomics, LR check, store). One wave per row. The 7 volume reads run kPF steps
-// ahead in a register ring; the scalar operands come from kChunk-step vector chunks.
-// ------------------------------------------------------------------------------------
-constexpr int kPF = 8;
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
+                                         uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
+                                         int xb, uint64_t* lds)
+{
+    using RS = RowSeg<DPL>;
+    constexpr int M = DPL / 2;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, w = tid >> 6;
+    const int r = lane >> 4, p = lane & 15;
+    const int j = 4 * w + r;                       // slot (line) of this row of lanes
+    const int rx = dir_rx(dir), ry = dir_ry(dir);
+    int s0, s1;
+    if (rx == 0) { s0 = 0; s1 = g.H; }
+    else if (rx > 0) { s0 = max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = min(g.H, g.maxX1 - xb); }
+    else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + kColsPerWG - g.minX1); }
+    if (s0 >= s1) return;                          // uniform over the workgroup
+    uint32_t imask[M];
+    make_imask<DPL, EXACT>(p, g.D, imask);
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = (uint32_t)g.P2 * 0x10001u;
+    uint32_t Lr[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) Lr[i] = imask[i];
+    bool pv = false;
+    const bool lane_act = EXACT || p * DPL < g.D;
+    uint8_t* tr = trash + (tid & 63) * DPL;
+    const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
+
+    uint64_t* buf0 = lds;
+    uint64_t* buf1 = lds + RS::BUF;
+    uint64_t A[RS::NLOAD], B[RS::NLOAD];
+    seg_load<DPL>(A, cL, cR, g, rx, ry, xb, s0, tid);
+    seg_store<DPL>((s0 & 1) ? buf1 : buf0, A, tid);
+    seg_load<DPL>(A, cL, cR, g, rx, ry, xb, min(s0 + 1, s1 - 1), tid);
+    __syncthreads();
+
+    auto step = [&](int s, const uint64_t* bufc) {
+        const int x = xb + j + rx * s;
+        const bool valid = s < s1 && x >= g.minX1 && x < g.maxX1;
+        const int y = ry > 0 ? s : g.H - 1 - s;
+        const uint64_t cl = bufc[RS::NPAD + j];
+        uint32_t C[M], Labs[M];
+        pair_costs<DPL>(cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, C);
+#pragma unroll
+        for (int i = 0; i < M; i++) Lr[i] = pv ? Lr[i] : imask[i];      // path start: L = C
+        p16_step<DPL, EXACT>(Lr, C, P1P1, P2P2, imask, Labs);
+        uint8_t* dst = (valid && lane_act)
+            ? V + ((size_t)min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL : tr;
+        store_pairs<DPL>(dst, Labs);
+        pv = valid;
+    };
+    for (int s = s0; s < s1; s += 2) {
+        seg_load<DPL>(B, cL, cR, g, rx, ry, xb, min(s + 2, s1 - 1), tid);
+        step(s, (s & 1) ? buf1 : buf0);
+        seg_store<DPL>(((s + 1) & 1) ? buf1 : buf0, A, tid);
+        __syncthreads();
+        seg_load<DPL>(A, cL, cR, g, rx, ry, xb, min(s + 3, s1 - 1), tid);
+        step(s + 1, ((s + 1) & 1) ? buf1 : buf0);
+        seg_store<DPL>((s & 1) ? buf1 : buf0, B, tid);
+        __syncthreads();
+    }
+}
+
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restrict__ cL,
+                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
+                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl)
+{
+    __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
+    const int b = blockIdx.x;
+    int slot = 0;
+#pragma unroll
+    for (int i = 1; i < 8; i++) slot += b >= pl.blk_start[i] ? 1 : 0;
+    const int dir = slot_dir(slot);
+    const int lb = b - pl.blk_start[slot];
+    uint8_t* V = vols + (size_t)dir * vol_bytes;
+    uint8_t* trash = V + trash_off;
+    if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
+}
+
+// ====================================================================================
+// Sum of the 8 path volumes + WTA + uniqueness + subpixel + disp2 + LR check.
+// One workgroup (4 waves) per row; wave w takes pixel batches b = w, w+4, ... of kU
+// consecutive columns; lanes over d (lane l holds d = l*DPL64 .. +DPL64-1). The next
+// batch's 8 volume words are in flight while the current batch is reduced.
+// ====================================================================================
 constexpr int kU = 4;
 
 template <int DPL>
-__global__ __launch_bounds__(64) void k_census_final(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
-                                                     const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
-                                                     int16_t* __restrict__ out, size_t out_stride)
+__global__ __launch_bounds__(kWG) void k_census_wta(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
+                                                    int16_t* __restrict__ out, size_t out_stride)
 {
     using VT = typename LaneVec<DPL>::T;
-    extern __shared__ uint32_t lds_final[];
-    RowLds R(lds_final, g.W);
-    const int lane = threadIdx.x;
+    extern __shared__ uint32_t lds_wta[];
+    RowLds R(lds_wta, g.W);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int y = blockIdx.x;
     const bool active = lane * DPL < g.D;
-    R.init(g, lane);
-
-    const uint64_t* cLr = cL + (size_t)y * g.W;
-    const uint64_t* cRr = cR + (size_t)y * g.W;
+    R.init(g, tid, kWG);
     const uint8_t* vrow = vols + (size_t)y * g.width1 * g.D + (active ? lane * DPL : 0);
     const int n = g.width1;
-    uint64_t cr[DPL];
+    const int nb = (n + kU - 1) / kU;
+    auto load = [&](int bb, VT (&v)[kU][8]) {
 #pragma unroll
-    for (int k = 0; k < DPL; k++) cr[k] = cRr[max(g.maxX1 - 1 - g.minD - lane * DPL - k, 0)];
-    int Lp[DPL];
+        for (int u = 0; u < kU; u++) {
+            const int x1 = min(bb * kU + u, n - 1);
 #pragma unroll
-    for (int k = 0; k < DPL; k++) Lp[k] = kInf;
-    int mLp = 0;
-    bool pv = false;
-
-    VT buf[kPF][7];
-#pragma unroll
-    for (int u = 0; u < kPF; u++)
-#pragma unroll
-        for (int r = 0; r < 7; r++)
-            buf[u][r] = *(const VT*)(vrow + (size_t)r * vol_bytes + (size_t)(n - 1 - min(u, n - 1)) * g.D);
-    HChunk cur = hchunk_load(cLr, cRr, g, -1, 0, lane, 64 * DPL);
-
-    static_assert(kChunk % kPF == 0 && kPF % kU == 0, "chunk layout");
-    for (int c = 0; c * kChunk < n; c++) {
-        const HChunk nxt = hchunk_load(cLr, cRr, g, -1, c + 1, lane, 64 * DPL);
-#pragma unroll
-        for (int q = 0; q < kChunk / kU; q++) {
-            int S[kU][DPL];
-            int xs[kU];
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                const int j = q * kU + u;            // step within the chunk
-                const int slot = j % kPF;             // ring slot (static)
-                const int i = c * kChunk + j;
-                xs[u] = g.maxX1 - 1 - i;
-                VT v[7];
-#pragma unroll
-                for (int r = 0; r < 7; r++) v[r] = buf[slot][r];
-                const int ip = min(i + kPF, n - 1);
-#pragma unroll
-                for (int r = 0; r < 7; r++)
-                    buf[slot][r] = *(const VT*)(vrow + (size_t)r * vol_bytes + (size_t)(n - 1 - ip) * g.D);
-                // ---- dir 7 recurrence ----
-                const uint64_t cl = readlane64(cur.cl, j);
-                const uint64_t inc = readlane64(cur.inc, j);
-                int cost[DPL], L[DPL];
-#pragma unroll
-                for (int k = 0; k < DPL; k++) cost[k] = popc64(cl ^ cr[k]);
-                const int lmin = path_step<DPL>(cost, Lp, mLp, pv, lane, g.D, g.P1, g.P2, L);
-                mLp = wave_min(lmin);
-#pragma unroll
-                for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-                pv = true;
-                const uint64_t nw = dpp_shl1_u64(cr[0], inc);            // slide the window to x-1
-#pragma unroll
-                for (int k = 0; k < DPL - 1; k++) cr[k] = cr[k + 1];
-                cr[DPL - 1] = nw;
-                // ---- S = L7 + 7 stored paths ----
-#pragma unroll
-                for (int k = 0; k < DPL; k++) {
-                    int sum = L[k];
-#pragma unroll
-                    for (int r = 0; r < 7; r++) sum += (int)((v[r] >> (8 * k)) & 0xFF);
-                    S[u][k] = active && (lane * DPL + k) < g.D ? sum : kInf;
-                }
-            }
-            const int nvalid = min(max(n - (c * kChunk + q * kU), 0), kU);
-            wta_batch<DPL, kU>(S, lane, xs, nvalid, g, R.drow, R.bst, R.mins);
+            for (int r = 0; r < 8; r++) v[u][r] = *(const VT*)(vrow + (size_t)r * vol_bytes + (size_t)x1 * g.D);
         }
-        cur = nxt;
+    };
+    VT cur[kU][8], nxt[kU][8];
+    load(min(w, nb - 1), cur);
+    for (int bb = w; bb < nb; bb += 4) {
+        load(min(bb + 4, nb - 1), nxt);
+        int S[kU][DPL], xs[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            xs[u] = g.minX1 + bb * kU + u;
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                int sum = 0;
+#pragma unroll
+                for (int r = 0; r < 8; r++) sum += (int)((cur[u][r] >> (8 * k)) & 0xFF);
+                S[u][k] = active && (lane * DPL + k) < g.D ? sum : kInf;
+            }
+        }
+        wta_batch<DPL, kU>(S, lane, xs, min(n - bb * kU, kU), g, R.drow, R.bst, R.mins);
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+#pragma unroll
+            for (int r = 0; r < 8; r++) cur[u][r] = nxt[u][r];
     }
-    row_finish(g, lane, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+    row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
 // ------------------------------------------------------------------------------------
@@ -378,59 +411,71 @@ hipError_t launch_census(const uint8_t* L, const uint8_t* R, size_t stride, int 
     return hipGetLastError();
 }
 
-static int dpl_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : D <= 256 ? 4 : 8; }
+static int dpl16_for(int D) { return D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
+static int dpl64_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : D <= 256 ? 4 : 8; }
 
-PathLaunch make_path_launch(const Geom& g, int only_dir)
+PathLaunch16 make_path_launch16(const Geom& g, int only_dir)
 {
-    PathLaunch pl{};
+    PathLaunch16 pl{};
     int acc = 0;
-    for (int dir = 0; dir < 7; dir++) {
-        pl.blk_start[dir] = acc;
-        int nb = 0;
-        if (dir < 6) {
+    for (int slot = 0; slot < 8; slot++) {
+        const int dir = slot_dir(slot);
+        pl.blk_start[slot] = acc;
+        int nb;
+        if (dir >= 6) {
+            nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
+        } else {
             const int rx = dir_rx(dir);
             const int lo = g.minX1 - (rx > 0 ? g.H - 1 : 0);
             const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
             pl.xb_lo[dir] = lo;
-            nb = (hi - lo + kG - 1) / kG;
-        } else {
-            nb = g.H;
+            nb = (hi - lo + kColsPerWG - 1) / kColsPerWG;
         }
         if (only_dir >= 0 && dir != only_dir) nb = 0;
         acc += nb;
     }
-    pl.blk_start[7] = acc;
+    pl.blk_start[8] = acc;
     return pl;
 }
 
-// Each volume slice is vol_bytes long: H*width1*D cells followed by a kTrashBytes trash
-// slot (see the memory-op discipline note above).
+template <int DPL>
+static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
+                             size_t trash_off, const Geom& g, const PathLaunch16& pl, hipStream_t st)
+{
+    dim3 grid(pl.blk_start[8]), block(kWG);
+    if (g.D == 16 * DPL)
+        hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl);
+    else
+        hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl);
+}
+
+// Each volume slice is vol_bytes long: H*width1*D cells followed by a trash slot.
 hipError_t launch_census_paths(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
                                const Geom& g, int only_dir, hipStream_t st)
 {
-    PathLaunch pl = make_path_launch(g, only_dir);
-    if (pl.blk_start[7] == 0) return hipSuccess;
+    PathLaunch16 pl = make_path_launch16(g, only_dir);
+    if (pl.blk_start[8] == 0) return hipSuccess;
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
-    dim3 grid(pl.blk_start[7]), block(64);
-    switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_census_paths<1>, grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl); break;
-    case 2: hipLaunchKernelGGL(k_census_paths<2>, grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl); break;
-    case 4: hipLaunchKernelGGL(k_census_paths<4>, grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl); break;
-    default: hipLaunchKernelGGL(k_census_paths<8>, grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl); break;
+    switch (dpl16_for(g.D)) {
+    case 2: launch_paths_dpl<2>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
+    case 4: launch_paths_dpl<4>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
+    case 8: launch_paths_dpl<8>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
+    case 16: launch_paths_dpl<16>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
+    default: launch_paths_dpl<32>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_census_final(const uint64_t* cL, const uint64_t* cR, const uint8_t* vols, size_t vol_bytes,
-                               const Geom& g, int16_t* out, size_t out_stride, hipStream_t st)
+hipError_t launch_census_wta(const uint8_t* vols, size_t vol_bytes, const Geom& g, int16_t* out, size_t out_stride,
+                             hipStream_t st)
 {
-    dim3 grid(g.H), block(64);
+    dim3 grid(g.H), block(kWG);
     const size_t lds = RowLds::bytes(g.W);
-    switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_census_final<1>, grid, block, lds, st, cL, cR, vols, vol_bytes, g, out, out_stride); break;
-    case 2: hipLaunchKernelGGL(k_census_final<2>, grid, block, lds, st, cL, cR, vols, vol_bytes, g, out, out_stride); break;
-    case 4: hipLaunchKernelGGL(k_census_final<4>, grid, block, lds, st, cL, cR, vols, vol_bytes, g, out, out_stride); break;
-    default: hipLaunchKernelGGL(k_census_final<8>, grid, block, lds, st, cL, cR, vols, vol_bytes, g, out, out_stride); break;
+    switch (dpl64_for(g.D)) {
+    case 1: hipLaunchKernelGGL(k_census_wta<1>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
+    case 2: hipLaunchKernelGGL(k_census_wta<2>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
+    case 4: hipLaunchKernelGGL(k_census_wta<4>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
+    default: hipLaunchKernelGGL(k_census_wta<8>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
     }
     return hipGetLastError();
 }

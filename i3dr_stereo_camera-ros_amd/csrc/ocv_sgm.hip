@@ -211,7 +211,7 @@ __global__ __launch_bounds__(64) void k_ocv_wta(const int16_t* __restrict__ vols
     extern __shared__ uint32_t lds_ocv[];
     RowLds R(lds_ocv, g.W);
     const int lane = threadIdx.x, y = blockIdx.x;
-    R.init(g, lane);
+    R.init(g, lane, 64);
     for (int i0 = 0; i0 < g.width1; i0 += 4) {
         int S[4][DPL], xs[4], nvalid = 0;
 #pragma unroll
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64) void k_ocv_wta(const int16_t* __restrict__ vols
         }
         wta_batch<DPL, 4>(S, lane, xs, nvalid, g, R.drow, R.bst, R.mins);
     }
-    row_finish(g, lane, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+    row_finish(g, lane, 64, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
 // ------------------------------------------------------------------------------------

@@ -22,8 +22,7 @@
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
 hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, int, hipStream_t);
-hipError_t launch_census_final(const uint64_t*, const uint64_t*, const uint8_t*, size_t, const Geom&, int16_t*,
-                               size_t, hipStream_t);
+hipError_t launch_census_wta(const uint8_t*, size_t, const Geom&, int16_t*, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -198,7 +197,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
         l.cL = take(WH * 8);
         l.cR = take(WH * 8);
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
-        l.vols = take(l.vol_bytes * 7);
+        l.vols = take(l.vol_bytes * 8);
     } else {
         l.planes = take(WH * 4);
         l.bufA = take(cells * 2);
@@ -262,10 +261,10 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         uint8_t* vols = (uint8_t*)(ws + l.vols);
         rec.begin("census", 2 * WH + 16 * WH);
         HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
-        rec.begin("paths7", 7 * cells);
+        rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, -1, st), "paths");
-        rec.begin("final_wta_lr", 7 * cells + 2 * WH);
-        HIP_TRY(sgm::launch_census_final(cL, cR, vols, l.vol_bytes, g, dst, dst_stride, st), "final");
+        rec.begin("wta_lr", 8 * cells + 2 * WH);
+        HIP_TRY(sgm::launch_census_wta(vols, l.vol_bytes, g, dst, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -552,7 +551,7 @@ int sgm_debug_census(sgm_handle* h, const uint8_t* img, int W, int H, size_t str
 int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int dir,
                           uint8_t* vol)
 {
-    if (!h || !L || !R || !vol || dir < 0 || dir > 6) return SGM_ERR_ARG;
+    if (!h || !L || !R || !vol || dir < 0 || dir > 7) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (h->params.mode != SGM_MODE_CENSUS8) return fail(h, SGM_ERR_PARAM, "census mode required");
     Geom g;

@@ -8,7 +8,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace sgm {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__host__ __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 constexpr int kInf = 0x3FFF;  // > any u8 path cost and any census S (<= 8*255)
 
@@ -148,7 +159,8 @@ __device__ __forceinline__ void wta_batch(const int (&S)[U][DPL], int lane, cons
         d16[u] = best[u] * 16 + (use ? tdiv((sm - sp) * 16 + den, 2 * den) : 0);
     }
     // lane u stores pixel u; every other lane (and pixels u >= nvalid) hits its own dummy
-    // slot at index W + lane, so the LDS stores need no exec-masked branch.
+    // slot at index W + lane, so the LDS stores need no exec-masked branch. (Dummy slots are
+    // shared by the waves of a workgroup: their content is never read.)
     int x = g.W + lane, b = -1, m = 32767, dv = 0, keep = 1;
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -174,11 +186,11 @@ __device__ __forceinline__ void wta_batch(const int (&S)[U][DPL], int lane, cons
 //     differ by more than disp12.
 //  3. store of the full row (columns outside [minX1, maxX1) stay invalid).
 // `key` needs W uint32; `d2` may alias `mins` (mins is dead after step 1).
-__device__ __forceinline__ void row_finish(const Geom& g, int lane, const int16_t* drow, const int16_t* bst,
+__device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, const int16_t* drow, const int16_t* bst,
                                            const uint16_t* mins, uint32_t* key, int16_t* d2, int16_t* orow)
 {
     __syncthreads();
-    for (int x = g.minX1 + lane; x < g.maxX1; x += 64) {
+    for (int x = g.minX1 + tid; x < g.maxX1; x += nthr) {
         const int b = bst[x];
         const int m = mins[x];
         if (b >= 0 && m < 32767) {
@@ -187,12 +199,12 @@ __device__ __forceinline__ void row_finish(const Geom& g, int lane, const int16_
         }
     }
     __syncthreads();
-    for (int x2 = lane; x2 < g.W; x2 += 64) {
+    for (int x2 = tid; x2 < g.W; x2 += nthr) {
         const uint32_t k = key[x2];
         d2[x2] = (int16_t)(k == 0xFFFFFFFFu ? g.invalid : bst[0xFFFF - (int)(k & 0xFFFF)] + g.minD);
     }
     __syncthreads();
-    for (int x = lane; x < g.W; x += 64) {
+    for (int x = tid; x < g.W; x += nthr) {
         int d1 = drow[x];
         if (g.lr && d1 != g.invalid) {
             const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
@@ -216,13 +228,55 @@ struct RowLds {
         bst = drow + W + 64;
         mins = (uint16_t*)(bst + W + 64);
     }
-    __device__ void init(const Geom& g, int lane) {
-        for (int x = lane; x < g.W; x += 64) {
+    __device__ void init(const Geom& g, int tid, int nthr) {
+        for (int x = tid; x < g.W; x += nthr) {
             key[x] = 0xFFFFFFFFu; drow[x] = (int16_t)g.invalid; bst[x] = -1; mins[x] = 32767;
         }
         __syncthreads();
     }
 };
+
+// ---- packed u16x2 arithmetic (v_pk_*_u16): two path costs per 32-bit register ----------
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2_t as_v2(uint32_t v) { return __builtin_bit_cast(u16x2_t, v); }
+__device__ __forceinline__ uint32_t as_u(u16x2_t v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_min(as_v2(a), as_v2(b))); }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u(as_v2(a) + as_v2(b)); }
+__device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_add_sat(as_v2(a), as_v2(b))); }
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) { return as_u(as_v2(a) - as_v2(b)); }
+// (hi:lo) >> 16 — e.g. alignbit16(x, y) = (x.lo, y.hi) as (hi, lo) halves
+__device__ __forceinline__ uint32_t alignbit16(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbit(hi, lo, 16); }
+
+// DPP inside 16-lane rows (lanes outside the row read `old`)
+__device__ __forceinline__ uint32_t row_shr1(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x111, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t row_shl1(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x101, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint64_t row_shr1_u64(uint64_t v, uint64_t old) {
+    return ((uint64_t)row_shr1((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) | row_shr1((uint32_t)v, (uint32_t)old);
+}
+__device__ __forceinline__ uint64_t row_shl1_u64(uint64_t v, uint64_t old) {
+    return ((uint64_t)row_shl1((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) | row_shl1((uint32_t)v, (uint32_t)old);
+}
+// unsigned min over the 16 lanes of each row, result in every lane of the row
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));    // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));    // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, true));   // row_ror:4
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, true));   // row_ror:8
+    return v;
+}
+// broadcast lane J of each 16-lane row (ds_swizzle bit-mask mode: and 0x10, or J)
+template <int J>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x10 | (J << 5));
+}
+template <int J>
+__device__ __forceinline__ uint64_t row_bcast_u64(uint64_t v) {
+    return ((uint64_t)row_bcast<J>((uint32_t)(v >> 32)) << 32) | row_bcast<J>((uint32_t)v);
+}
 
 // Pack DPL u8 path costs of one lane into the per-lane store word.
 template <int DPL> struct LaneVec;

@@ -137,7 +137,7 @@ double sgm_stage_bytes(const sgm_handle* h, int i);
 /* 9x7 census codes of one image (host buffers; out: W x H uint64, row-major).             */
 int  sgm_debug_census(sgm_handle* h, const uint8_t* img, int width, int height,
                       size_t stride, uint64_t* out);
-/* Census mode: u8 path-cost volume of direction `dir` (0..6; see DESIGN.md for the order),
+/* Census mode: u8 path-cost volume of direction `dir` (0..7; see DESIGN.md for the order),
  * layout [H][width1][D]. Runs census + that direction only.                               */
 int  sgm_debug_census_path(sgm_handle* h, const uint8_t* left, const uint8_t* right,
                            int width, int height, size_t stride, int dir, uint8_t* vol);

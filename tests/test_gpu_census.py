@@ -21,7 +21,7 @@ def test_census_codes(engine, oracle, shape):
 
 
 @pytest.mark.parametrize("D,minD", [(16, 0), (32, -7), (64, 3), (128, 0), (256, 0), (512, 0), (48, 2), (80, -3)])
-@pytest.mark.parametrize("dirn", range(7))
+@pytest.mark.parametrize("dirn", range(8))
 def test_census_path_volumes(engine, oracle, synth, pkg, dirn, D, minD):
     h = 23
     w = max(D + minD, 0) + 57
@@ -177,5 +177,5 @@ def test_profiling_stage_times(engine, pkg, synth):
     st = engine.stage_times()
     engine.set_profiling(False)
     names = [s[0] for s in st]
-    assert names[:3] == ["census", "paths7", "final_wta_lr"]
+    assert names[:3] == ["census", "paths8", "wta_lr"]
     assert all(t >= 0 for _, t, _ in st) and all(b > 0 for _, _, b in st)
