@@ -340,6 +340,9 @@ __global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restri
     const int lb = b - pl.blk_start[slot];
     uint8_t* V = vols + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
+    // The two horizontal scans are the longest dependency chains (width1 sequential steps):
+    // raise their wave priority so they issue first and the row sweeps fill the gaps.
+    if (dir >= 6) __builtin_amdgcn_s_setprio(2);
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
@@ -347,55 +350,126 @@ __global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restri
 
 // ====================================================================================
 // Sum of the 8 path volumes + WTA + uniqueness + subpixel + disp2 + LR check.
-// One workgroup (4 waves) per row; wave w takes pixel batches b = w, w+4, ... of kU
-// consecutive columns; lanes over d (lane l holds d = l*DPL64 .. +DPL64-1). The next
-// batch's 8 volume words are in flight while the current batch is reduced.
+// One workgroup (4 waves) per image row. 16 lanes per pixel (the P16 layout of the path
+// engine): each wave-instruction covers 4 consecutive pixels, lane p of a row holds
+// d = p*DPL .. p*DPL + DPL-1, loaded as one DPL-byte vector per volume (coalesced).
+//  * S = sum of 8 u8 volumes in SWAR u16 pairs: even bytes (w & 0x00FF00FF) and odd bytes
+//    (perm) accumulate separately, <= 8*255 per half, so 32-bit adds never carry over.
+//  * best and minS in ONE 16-lane min-reduction over key = S*512 + d (first minimal d).
+//  * uniqueness: a second key-min over d outside [best-1, best+1].
+//  * S[best-1], S[best+1] for the subpixel fit: read back from a per-row LDS slice.
+// Results go to the row's LDS arrays; row_finish() does disp2 (LDS atomics) + LR + store.
 // ====================================================================================
-constexpr int kU = 4;
+template <int DPL>
+struct WVec;
+template <> struct WVec<2> { using T = uint16_t; static constexpr int NW = 1; };
+template <> struct WVec<4> { using T = uint32_t; static constexpr int NW = 1; };
+template <> struct WVec<8> { using T = uint2; static constexpr int NW = 2; };
+template <> struct WVec<16> { using T = uint4; static constexpr int NW = 4; };
+template <> struct WVec<32> { using T = uint4; static constexpr int NW = 4; };   // two vectors
 
 template <int DPL>
-__global__ __launch_bounds__(kWG) void k_census_wta(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
-                                                    int16_t* __restrict__ out, size_t out_stride)
+__device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 3) / 4])
 {
-    using VT = typename LaneVec<DPL>::T;
+    if constexpr (DPL == 2) { wd[0] = *(const uint16_t*)src; }
+    else if constexpr (DPL == 4) { wd[0] = *(const uint32_t*)src; }
+    else if constexpr (DPL == 8) { const uint2 v = *(const uint2*)src; wd[0] = v.x; wd[1] = v.y; }
+    else {
+#pragma unroll
+        for (int q = 0; q < DPL / 16; q++) {
+            const uint4 v = ((const uint4*)src)[q];
+            wd[4 * q] = v.x; wd[4 * q + 1] = v.y; wd[4 * q + 2] = v.z; wd[4 * q + 3] = v.w;
+        }
+    }
+}
+
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
+                                                      int16_t* __restrict__ out, size_t out_stride)
+{
+    constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
     extern __shared__ uint32_t lds_wta[];
-    RowLds R(lds_wta, g.W);
+    uint32_t* sl = lds_wta;                       // 4 waves x 4 rows x 16*DPL u16 S values
+    RowLds R(lds_wta + kWG * DPL / 2, g.W);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane >> 4, p = lane & 15;
     const int y = blockIdx.x;
-    const bool active = lane * DPL < g.D;
     R.init(g, tid, kWG);
-    const uint8_t* vrow = vols + (size_t)y * g.width1 * g.D + (active ? lane * DPL : 0);
+    const bool lane_act = EXACT || p * DPL < g.D;
+    const uint8_t* vrow = vols + (size_t)y * g.width1 * g.D + (lane_act ? p * DPL : 0);
+    uint32_t* srow = sl + (w * 4 + r) * 8 * DPL;
     const int n = g.width1;
-    const int nb = (n + kU - 1) / kU;
-    auto load = [&](int bb, VT (&v)[kU][8]) {
+    const int nq = (n + 3) / 4;
+    auto load = [&](int q, uint32_t (&v)[8][NWD]) {
+        const int x1 = min(4 * q + r, n - 1);
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int x1 = min(bb * kU + u, n - 1);
-#pragma unroll
-            for (int r = 0; r < 8; r++) v[u][r] = *(const VT*)(vrow + (size_t)r * vol_bytes + (size_t)x1 * g.D);
-        }
+        for (int vv = 0; vv < 8; vv++) wload<DPL>(vrow + (size_t)vv * vol_bytes + (size_t)x1 * g.D, v[vv]);
     };
-    VT cur[kU][8], nxt[kU][8];
-    load(min(w, nb - 1), cur);
-    for (int bb = w; bb < nb; bb += 4) {
-        load(min(bb + 4, nb - 1), nxt);
-        int S[kU][DPL], xs[kU];
+    uint32_t cur[8][NWD], nxt[8][NWD];
+    load(min(w, nq - 1), cur);
+    for (int q = w; q < nq; q += 4) {
+        load(min(q + 4, nq - 1), nxt);
+        // ---- S in u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]) ----
+        uint32_t E[NWD], O[NWD];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            xs[u] = g.minX1 + bb * kU + u;
+        for (int j = 0; j < NWD; j++) {
+            uint32_t e = 0, o = 0;
 #pragma unroll
-            for (int k = 0; k < DPL; k++) {
-                int sum = 0;
-#pragma unroll
-                for (int r = 0; r < 8; r++) sum += (int)((cur[u][r] >> (8 * k)) & 0xFF);
-                S[u][k] = active && (lane * DPL + k) < g.D ? sum : kInf;
+            for (int vv = 0; vv < 8; vv++) {
+                e += cur[vv][j] & 0x00FF00FFu;
+                o += __builtin_amdgcn_perm(0u, cur[vv][j], 0x0c030c01u);
             }
+            E[j] = e;
+            O[j] = o;
         }
-        wta_batch<DPL, kU>(S, lane, xs, min(n - bb * kU, kU), g, R.drow, R.bst, R.mins);
+        // ---- keys, min -> (minS, best) ----
+        uint32_t S[4 * NWD], key[4 * NWD];
+        uint32_t kmin = 0xFFFFFFFFu;
 #pragma unroll
-        for (int u = 0; u < kU; u++)
+        for (int j = 0; j < NWD; j++) {
+            S[4 * j + 0] = E[j] & 0xFFFFu; S[4 * j + 2] = E[j] >> 16;
+            S[4 * j + 1] = O[j] & 0xFFFFu; S[4 * j + 3] = O[j] >> 16;
+        }
 #pragma unroll
-            for (int r = 0; r < 8; r++) cur[u][r] = nxt[u][r];
+        for (int k = 0; k < DPL; k++) {
+            const int d = p * DPL + k;
+            if (!EXACT && d >= g.D) S[k] = 0xFFFFu;
+            key[k] = (S[k] << 9) | (uint32_t)(d & 511);
+            kmin = min(kmin, key[k]);
+        }
+        kmin = row_min_u32(kmin);
+        const int best = (int)(kmin & 511u);
+        const int minS = (int)(kmin >> 9);
+        // ---- uniqueness: min S over d outside [best-1, best+1] ----
+        uint32_t k2 = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = p * DPL + k;
+            k2 = ((unsigned)(d - best + 1) <= 2u || (!EXACT && d >= g.D)) ? k2 : min(k2, key[k]);
+        }
+        k2 = row_min_u32(k2);
+        const bool rej = k2 != 0xFFFFFFFFu && (int)(k2 >> 9) * (100 - g.uniq) < minS * 100;
+        // ---- subpixel: S[best-1], S[best+1] through the row's LDS slice ----
+        // (one access type, u32, for the stores and the loads: no type-based reordering)
+#pragma unroll
+        for (int k = 0; k < DPL; k += 2) srow[(p * DPL + k) >> 1] = (S[k + 1] << 16) | S[k];
+        const int bm = max(best - 1, 0), bp = min(best + 1, 16 * DPL - 1);
+        const int sm = (int)((srow[bm >> 1] >> ((bm & 1) * 16)) & 0xFFFFu);
+        const int sp = (int)((srow[bp >> 1] >> ((bp & 1) * 16)) & 0xFFFFu);
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int d16 = best * 16 + (use ? tdiv((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        // ---- results: lane 0 of each row writes its pixel, the others hit dummy slots ----
+        const int x1 = 4 * q + r;
+        const bool wr = p == 0 && x1 < n;
+        const int x = wr ? g.minX1 + x1 : g.W + lane;
+        R.bst[x] = (int16_t)(rej ? -1 : best);
+        R.mins[x] = (uint16_t)minS;
+        R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
+#pragma unroll
+        for (int vv = 0; vv < 8; vv++)
+#pragma unroll
+            for (int j = 0; j < NWD; j++) cur[vv][j] = nxt[vv][j];
     }
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
@@ -412,7 +486,6 @@ hipError_t launch_census(const uint8_t* L, const uint8_t* R, size_t stride, int 
 }
 
 static int dpl16_for(int D) { return D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
-static int dpl64_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : D <= 256 ? 4 : 8; }
 
 PathLaunch16 make_path_launch16(const Geom& g, int only_dir)
 {
@@ -466,16 +539,27 @@ hipError_t launch_census_paths(const uint64_t* cL, const uint64_t* cR, uint8_t* 
     return hipGetLastError();
 }
 
+template <int DPL>
+static void launch_wta_dpl(const uint8_t* vols, size_t vol_bytes, const Geom& g, int16_t* out, size_t out_stride,
+                           hipStream_t st)
+{
+    dim3 grid(g.H), block(kWG);
+    const size_t lds = (size_t)kWG * DPL * 2 + RowLds::bytes(g.W);
+    if (g.D == 16 * DPL)
+        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, vols, vol_bytes, g, out, out_stride);
+    else
+        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, vols, vol_bytes, g, out, out_stride);
+}
+
 hipError_t launch_census_wta(const uint8_t* vols, size_t vol_bytes, const Geom& g, int16_t* out, size_t out_stride,
                              hipStream_t st)
 {
-    dim3 grid(g.H), block(kWG);
-    const size_t lds = RowLds::bytes(g.W);
-    switch (dpl64_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_census_wta<1>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
-    case 2: hipLaunchKernelGGL(k_census_wta<2>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
-    case 4: hipLaunchKernelGGL(k_census_wta<4>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
-    default: hipLaunchKernelGGL(k_census_wta<8>, grid, block, lds, st, vols, vol_bytes, g, out, out_stride); break;
+    switch (dpl16_for(g.D)) {
+    case 2: launch_wta_dpl<2>(vols, vol_bytes, g, out, out_stride, st); break;
+    case 4: launch_wta_dpl<4>(vols, vol_bytes, g, out, out_stride, st); break;
+    case 8: launch_wta_dpl<8>(vols, vol_bytes, g, out, out_stride, st); break;
+    case 16: launch_wta_dpl<16>(vols, vol_bytes, g, out, out_stride, st); break;
+    default: launch_wta_dpl<32>(vols, vol_bytes, g, out, out_stride, st); break;
     }
     return hipGetLastError();
 }
