@@ -11,6 +11,9 @@
 // stored); S never touches HBM.
 #include "sgm_device.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace sgm {
 
 // ------------------------------------------------------------------------------------
@@ -57,7 +60,9 @@ __global__ __launch_bounds__(256) void k_census9x7(const uint8_t* __restrict__ L
 // which equals SGM's C + min(Lp, Lp+-1 + P1, minLp + P2) - minLp exactly (all values
 // <= 255 because C <= 62 and P2 <= 193). min over D is a 4-step DPP reduction inside the
 // row; the d-1 / d+1 neighbours are v_alignbit of adjacent registers plus one row_shr /
-// row_shl DPP for the lane boundary. Entries with d >= D are forced to 0xFFFF.
+// row_shl DPP for the lane boundary. Values are kept as biased-f16 bit patterns (see
+// p16_step) so that one v_pk_minimum3_f16 does two of the mins; entries with d >= D are
+// forced to a large finite pattern.
 //
 // Memory-op discipline: gfx950 counts loads and stores on one in-order vmcnt and hipcc
 // only emits counted waits when every path through a loop body issues the same VMEM ops.
@@ -85,57 +90,95 @@ __device__ __forceinline__ void store_pairs(uint8_t* dst, const uint32_t (&L)[DP
     }
 }
 
-// Hamming costs of the lane's DPL disparities as u16 pairs; crk(k) = right code of d = p*DPL + k
-template <int DPL, typename F>
-__device__ __forceinline__ void pair_costs(uint64_t cl, F crk, uint32_t (&C)[DPL / 2])
+// Path-cost arithmetic in the "biased f16" domain. A cost v in [0, 1024) is held as the u16
+// bit pattern kBase + v (kBase = 0x6400 = f16 1024.0). In that binade the f16 ulp is 1, so
+//  * the bit pattern is exactly the f16 value 1024 + v: f16 min/minimum3 on patterns = integer
+//    min on v (v_pk_minimum3_f16 gives a packed 3-way min in one instruction), and
+//  * integer adds/subtracts of small amounts on the pattern (v_pk_add_u16, v_bcnt's
+//    accumulator) are exact, and the low byte of a pattern is v itself (v <= 255).
+// "Infinite" entries (d >= D, lane edges) are kInfP = 0x7000 (f16 8192): finite, so no NaN
+// can appear, and above every real value (<= kBase + 255 + P1 + 62).
+constexpr uint32_t kBaseP = 0x6400u, kBaseP2 = 0x64006400u;
+constexpr uint32_t kInfP = 0x7000u, kInfP2 = 0x70007000u;
+
+__device__ __forceinline__ uint32_t pk_min3_p(uint32_t a, uint32_t b, uint32_t c)
 {
-#pragma unroll
-    for (int i = 0; i < DPL / 2; i++)
-        C[i] = (uint32_t)popc64(cl ^ crk(2 * i)) | ((uint32_t)popc64(cl ^ crk(2 * i + 1)) << 16);
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    const h2_t r = __builtin_elementwise_minimum(
+        __builtin_elementwise_minimum(__builtin_bit_cast(h2_t, a), __builtin_bit_cast(h2_t, b)), __builtin_bit_cast(h2_t, c));
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_max(as_v2(a), as_v2(b))); }
+
+// popcount(x) + acc (v_bcnt_u32_b32 with accumulator). Inline asm keeps the accumulator
+// chain as written: hipcc otherwise re-associates the adds into extra v_add3 / v_add_lshl.
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
+{
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+// acc + Hamming(a, b) of two 64-bit census codes: 2 xor + 2 bcnt
+__device__ __forceinline__ uint32_t ham_acc(uint64_t a, uint64_t b, uint32_t acc)
+{
+    const uint64_t x = a ^ b;
+    return bcnt_acc((uint32_t)(x >> 32), bcnt_acc((uint32_t)x, acc));
 }
 
-// One recurrence step of the lane's pairs. Lr: relative state in/out. Labs: absolute L.
-template <int DPL, bool EXACT>
-__device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], const uint32_t (&C)[DPL / 2], uint32_t P1P1,
-                                         uint32_t P2P2, const uint32_t (&imask)[DPL / 2], uint32_t (&Labs)[DPL / 2])
+// One recurrence step of the lane's pairs, costs computed on the fly:
+//   L(d) = C(d) + min(Lr(d), Lr(d-1) + P1, Lr(d+1) + P1, P2),  C(d) = Hamming(cl, crk(d))
+// Lr: relative state (patterns) in/out. Labs: absolute L (patterns) out.
+// Per pair: q = Lr + P1 (1), neighbour align (1), minimum3 (1), min P2 (1), 4 xor + 4 bcnt
+// + 1 shift-add for the two costs (the low cost rides on v_bcnt's accumulator), 1/2 for the
+// min reduction, 1 subtract.
+template <int DPL, bool EXACT, typename F>
+__device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F crk, uint32_t P1P1, uint32_t P2P2,
+                                         const uint32_t (&imask)[DPL / 2], uint32_t (&Labs)[DPL / 2])
 {
     constexpr int M = DPL / 2;
-    const uint32_t X = row_shr1(Lr[M - 1], 0xFFFFFFFFu);   // previous lane: its .hi is L(d0 - 1)
-    const uint32_t Y = row_shl1(Lr[0], 0xFFFFFFFFu);       // next lane: its .lo is L(d0 + DPL)
-    uint32_t mn = 0xFFFFFFFFu;
-    uint32_t Oprev = alignbit16(Lr[0], X);                  // (L(d-1), L(d)) for pair 0
+    uint32_t q[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) q[i] = pk_add(Lr[i], P1P1);
+    const uint32_t X = row_shr1(q[M - 1], kInfP2);        // previous lane: its .hi is q(d0 - 1)
+    const uint32_t Y = row_shl1(q[0], kInfP2);            // next lane: its .lo is q(d0 + DPL)
+    uint32_t Oprev = alignbit16(q[0], X);                 // (q(d-1), q(d)) for pair 0
 #pragma unroll
     for (int i = 0; i < M; i++) {
-        const uint32_t Onext = (i + 1 < M) ? alignbit16(Lr[i + 1], Lr[i]) : alignbit16(Y, Lr[M - 1]);
-        const uint32_t u = pk_adds(pk_min(Oprev, Onext), P1P1);
-        const uint32_t v = pk_min(pk_min(u, Lr[i]), P2P2);
-        uint32_t L = pk_add(v, C[i]);
-        if (!EXACT) L |= imask[i];
+        const uint32_t Onext = (i + 1 < M) ? alignbit16(q[i + 1], q[i]) : alignbit16(Y, q[M - 1]);
+        const uint32_t t = pk_min(pk_min3_p(Oprev, Onext, Lr[i]), P2P2);
+        const uint32_t c1 = ham_acc(cl, crk(2 * i + 1), 0u);
+        uint32_t L = ham_acc(cl, crk(2 * i), t) + (c1 << 16);
+        if (!EXACT) L = pk_max(L, imask[i]);
         Labs[i] = L;
-        mn = pk_min(mn, L);
         Oprev = Onext;
     }
-    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
+    uint32_t mn = Labs[0];
 #pragma unroll
-    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], mn);
+    for (int i = 1; i < M; i += 2) mn = (i + 1 < M) ? pk_min3_p(mn, Labs[i], Labs[i + 1]) : pk_min(mn, Labs[i]);
+    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
+    const uint32_t off = mn - kBaseP2;                    // pattern(L) - off = pattern(L - min)
+#pragma unroll
+    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], off);
 }
 
+// imask: kInfP in the halves with d >= D (0 elsewhere); start: the relative state of a
+// path's first pixel (L = C): kBase, or kInfP | kBase for d >= D.
 template <int DPL, bool EXACT>
-__device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL / 2])
+__device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL / 2], uint32_t (&start)[DPL / 2])
 {
 #pragma unroll
     for (int i = 0; i < DPL / 2; i++) {
         const int d = p * DPL + 2 * i;
-        imask[i] = EXACT ? 0u : ((d < D ? 0u : 0xFFFFu) | (d + 1 < D ? 0u : 0xFFFF0000u));
+        imask[i] = EXACT ? 0u : ((d < D ? 0u : kInfP) | (d + 1 < D ? 0u : kInfP << 16));
+        start[i] = imask[i] | kBaseP2;
     }
 }
 
 struct PathLaunch16 {
-    int blk_start[9];    // workgroups of launch slot i (order kSlotDir), blk_start[8] = total
-    int xb_lo[8];        // row sweeps: first base column of the direction
+    int xb_lo[6];        // row sweeps: first base column of the direction
 };
-// launch order: the two horizontal scans first (longest dependency chains), then rows
-__host__ __device__ constexpr int slot_dir(int i) { return i < 2 ? 6 + i : i - 2; }
+// Work list entry of k_census_paths16 (one per workgroup): dir << 24 | local block.
+__host__ __device__ constexpr uint32_t path_item(int dir, int lb) { return ((uint32_t)dir << 24) | (uint32_t)lb; }
 
 constexpr int kWG = 256;          // 4 waves
 constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
@@ -176,9 +219,9 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     const int yc = min(y, g.H - 1);
     const uint64_t* cLr = cL + (size_t)yc * g.W;
     const uint64_t* cRr = cR + (size_t)yc * g.W;
-    uint32_t imask[M];
-    make_imask<DPL, EXACT>(p, g.D, imask);
-    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = (uint32_t)g.P2 * 0x10001u;
+    uint32_t imask[M], start[M];
+    make_imask<DPL, EXACT>(p, g.D, imask, start);
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = ((uint32_t)g.P2 + kBaseP) * 0x10001u;
     const int n = g.width1;
     const int xfirst = DX > 0 ? g.minX1 : g.maxX1 - 1;
     uint64_t cr[DPL];                             // physical window registers
@@ -186,7 +229,7 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     for (int k = 0; k < DPL; k++) cr[k] = cRr[min(max(xfirst - g.minD - p * DPL - k, 0), g.W - 1)];
     uint32_t Lr[M];
 #pragma unroll
-    for (int i = 0; i < M; i++) Lr[i] = imask[i];
+    for (int i = 0; i < M; i++) Lr[i] = start[i];
     uint8_t* rowbase = V + (size_t)yc * g.width1 * g.D + p * DPL;
     uint8_t* tr = trash + lane * DPL;
     const bool lane_ok = rowok && (EXACT || p * DPL < g.D);
@@ -200,9 +243,9 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
             const uint64_t cl = row_bcast_u64<t % 16>(cur.cl);
             const uint64_t inj = row_bcast_u64<t % 16>(cur.inj);
             // logical window index k lives in physical register (k - t) (DX>0) / (k + t) (DX<0)
-            uint32_t C[M], Labs[M];
-            pair_costs<DPL>(cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; }, C);
-            p16_step<DPL, EXACT>(Lr, C, P1P1, P2P2, imask, Labs);
+            uint32_t Labs[M];
+            p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; },
+                                 P1P1, P2P2, imask, Labs);
             const int x1 = DX > 0 ? i : n - 1 - i;
             store_pairs<DPL>((lane_ok && i < n) ? rowbase + (size_t)x1 * g.D : tr, Labs);
             if constexpr (DX > 0) {
@@ -280,12 +323,12 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     else if (rx > 0) { s0 = max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = min(g.H, g.maxX1 - xb); }
     else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + kColsPerWG - g.minX1); }
     if (s0 >= s1) return;                          // uniform over the workgroup
-    uint32_t imask[M];
-    make_imask<DPL, EXACT>(p, g.D, imask);
-    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = (uint32_t)g.P2 * 0x10001u;
+    uint32_t imask[M], start[M];
+    make_imask<DPL, EXACT>(p, g.D, imask, start);
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = ((uint32_t)g.P2 + kBaseP) * 0x10001u;
     uint32_t Lr[M];
 #pragma unroll
-    for (int i = 0; i < M; i++) Lr[i] = imask[i];
+    for (int i = 0; i < M; i++) Lr[i] = start[i];
     bool pv = false;
     const bool lane_act = EXACT || p * DPL < g.D;
     uint8_t* tr = trash + (tid & 63) * DPL;
@@ -304,11 +347,10 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         const bool valid = s < s1 && x >= g.minX1 && x < g.maxX1;
         const int y = ry > 0 ? s : g.H - 1 - s;
         const uint64_t cl = bufc[RS::NPAD + j];
-        uint32_t C[M], Labs[M];
-        pair_costs<DPL>(cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, C);
+        uint32_t Labs[M];
 #pragma unroll
-        for (int i = 0; i < M; i++) Lr[i] = pv ? Lr[i] : imask[i];      // path start: L = C
-        p16_step<DPL, EXACT>(Lr, C, P1P1, P2P2, imask, Labs);
+        for (int i = 0; i < M; i++) Lr[i] = pv ? Lr[i] : start[i];      // path start: L = C
+        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2P2, imask, Labs);
         uint8_t* dst = (valid && lane_act)
             ? V + ((size_t)min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL : tr;
         store_pairs<DPL>(dst, Labs);
@@ -329,20 +371,15 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 template <int DPL, bool EXACT>
 __global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restrict__ cL,
                                                         const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
-                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl)
+                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
+                                                        const uint32_t* __restrict__ items)
 {
     __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
-    const int b = blockIdx.x;
-    int slot = 0;
-#pragma unroll
-    for (int i = 1; i < 8; i++) slot += b >= pl.blk_start[i] ? 1 : 0;
-    const int dir = slot_dir(slot);
-    const int lb = b - pl.blk_start[slot];
+    const uint32_t it = items[blockIdx.x];
+    const int dir = (int)(it >> 24);
+    const int lb = (int)(it & 0xFFFFFFu);
     uint8_t* V = vols + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
-    // The two horizontal scans are the longest dependency chains (width1 sequential steps):
-    // raise their wave priority so they issue first and the row sweeps fill the gaps.
-    if (dir >= 6) __builtin_amdgcn_s_setprio(2);
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
@@ -487,54 +524,83 @@ hipError_t launch_census(const uint8_t* L, const uint8_t* R, size_t stride, int 
 
 static int dpl16_for(int D) { return D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
-PathLaunch16 make_path_launch16(const Geom& g, int only_dir)
+PathLaunch16 make_path_launch16(const Geom& g)
 {
     PathLaunch16 pl{};
-    int acc = 0;
-    for (int slot = 0; slot < 8; slot++) {
-        const int dir = slot_dir(slot);
-        pl.blk_start[slot] = acc;
-        int nb;
-        if (dir >= 6) {
-            nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
-        } else {
-            const int rx = dir_rx(dir);
-            const int lo = g.minX1 - (rx > 0 ? g.H - 1 : 0);
-            const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
-            pl.xb_lo[dir] = lo;
-            nb = (hi - lo + kColsPerWG - 1) / kColsPerWG;
-        }
-        if (only_dir >= 0 && dir != only_dir) nb = 0;
-        acc += nb;
-    }
-    pl.blk_start[8] = acc;
+    for (int dir = 0; dir < 6; dir++) pl.xb_lo[dir] = g.minX1 - (dir_rx(dir) > 0 ? g.H - 1 : 0);
     return pl;
+}
+
+// Work list of one paths launch: every workgroup of every direction (only_dir >= 0: that
+// direction only), longest first, dealt out in a snake over rounds of n_slots workgroups.
+// The hardware hands consecutive workgroup ids to different CUs, so each CU ends up with a
+// mix of long (horizontal, vertical) and short (diagonal corner) work instead of several
+// long ones — the kernel's tail is the most loaded CU.
+int census_path_items(const Geom& g, int only_dir, int n_slots, uint32_t* out, int cap)
+{
+    struct Item { int len; uint32_t code; };
+    std::vector<Item> v;
+    const PathLaunch16 pl = make_path_launch16(g);
+    for (int dir = 0; dir < 8; dir++) {
+        if (only_dir >= 0 && dir != only_dir) continue;
+        if (dir >= 6) {
+            const int nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
+            for (int b = 0; b < nb; b++) v.push_back({g.width1, path_item(dir, b)});
+            continue;
+        }
+        const int rx = dir_rx(dir);
+        const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
+        const int nb = (hi - pl.xb_lo[dir] + kColsPerWG - 1) / kColsPerWG;
+        for (int b = 0; b < nb; b++) {
+            const int xb = pl.xb_lo[dir] + b * kColsPerWG;
+            int s0, s1;      // same step range as p16_rows
+            if (rx == 0) { s0 = 0; s1 = g.H; }
+            else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
+            else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + kColsPerWG - g.minX1); }
+            v.push_back({std::max(s1 - s0, 0), path_item(dir, b)});
+        }
+    }
+    const int n = (int)v.size();
+    if (!out) return n;
+    if (n > cap) return -1;
+    std::stable_sort(v.begin(), v.end(), [](const Item& a, const Item& b) { return a.len > b.len; });
+    n_slots = std::max(n_slots, 1);
+    for (int k = 0; k < n; k++) {
+        const int round = k / n_slots, i = k % n_slots;
+        const int in_round = std::min(n_slots, n - round * n_slots);
+        out[round * n_slots + ((round & 1) ? in_round - 1 - i : i)] = v[k].code;
+    }
+    return n;
 }
 
 template <int DPL>
 static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
-                             size_t trash_off, const Geom& g, const PathLaunch16& pl, hipStream_t st)
+                             size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
+                             int n_items, hipStream_t st)
 {
-    dim3 grid(pl.blk_start[8]), block(kWG);
+    dim3 grid(n_items), block(kWG);
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl);
+        hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl,
+                           items);
     else
-        hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl);
+        hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g,
+                           pl, items);
 }
 
 // Each volume slice is vol_bytes long: H*width1*D cells followed by a trash slot.
+// items: device copy of census_path_items() for this geometry (n_items entries).
 hipError_t launch_census_paths(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
-                               const Geom& g, int only_dir, hipStream_t st)
+                               const Geom& g, const uint32_t* items, int n_items, hipStream_t st)
 {
-    PathLaunch16 pl = make_path_launch16(g, only_dir);
-    if (pl.blk_start[8] == 0) return hipSuccess;
+    if (n_items <= 0) return hipSuccess;
+    const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
-    case 2: launch_paths_dpl<2>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
-    case 4: launch_paths_dpl<4>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
-    case 8: launch_paths_dpl<8>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
-    case 16: launch_paths_dpl<16>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
-    default: launch_paths_dpl<32>(cL, cR, vols, vol_bytes, trash_off, g, pl, st); break;
+    case 2: launch_paths_dpl<2>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 4: launch_paths_dpl<4>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 8: launch_paths_dpl<8>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 16: launch_paths_dpl<16>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    default: launch_paths_dpl<32>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
     }
     return hipGetLastError();
 }

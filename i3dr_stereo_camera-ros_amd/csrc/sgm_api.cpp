@@ -21,7 +21,9 @@
 
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
-hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, int, hipStream_t);
+int census_path_items(const Geom&, int, int, uint32_t*, int);
+hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, const uint32_t*, int,
+                               hipStream_t);
 hipError_t launch_census_wta(const uint8_t*, size_t, const Geom&, int16_t*, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
@@ -105,6 +107,10 @@ struct sgm_handle {
     const char* stage_name[SGM_MAX_STAGES] = {};
     double stage_bytes[SGM_MAX_STAGES] = {};
     std::vector<sgm_handle*> sub;  // per-device handles for sgm_match_batch
+    int n_cu = 0;                  // compute units of the device (path work-list dealing)
+    uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
+    int items_cap = 0;
+    std::string items_key;         // geometry + workspace the device copy belongs to
 };
 
 namespace {
@@ -130,6 +136,7 @@ int ensure_stream(sgm_handle* h)
 {
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
     if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!h->n_cu) HIP_TRY(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->device), "attr");
     return SGM_OK;
 }
 
@@ -152,6 +159,7 @@ sgm_handle::ProfRec* next_prof(sgm_handle* h)
 int ensure_ws(sgm_handle* h, size_t bytes)
 {
     if (h->ws.size >= bytes) return SGM_OK;
+    h->items_key.clear();          // contents (the path work list) do not survive
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
         (void)hipFree(h->ws.base);
@@ -180,6 +188,7 @@ int ensure_pin(sgm_handle* h, size_t bytes)
 // Workspace carve-up for one geometry. Offsets are 256-B aligned.
 struct Layout {
     size_t cL = 0, cR = 0, vols = 0, vol_bytes = 0;       // census
+    size_t items = 0; int n_items = 0;                     // census path work list
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovol_elems = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0;                      // host-API staging
@@ -198,6 +207,10 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
         l.cR = take(WH * 8);
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
         l.vols = take(l.vol_bytes * 8);
+        if (g.width1 > 0) {
+            l.n_items = sgm::census_path_items(g, -1, 1, nullptr, 0);
+            l.items = take((size_t)l.n_items * 4);
+        }
     } else {
         l.planes = take(WH * 4);
         l.bufA = take(cells * 2);
@@ -235,6 +248,32 @@ struct StageRec {
     }
 };
 
+// Device work list of the census path launch for (g, only_dir), uploaded on `st` when the
+// geometry or the workspace changed. Returns the entry count (< 0: error).
+int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, hipStream_t st, const uint32_t** dev)
+{
+    uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items);
+    *dev = d;
+    char key[160];
+    snprintf(key, sizeof key, "%d %d %d %d %d %d %p", g.W, g.H, g.D, g.minD, only_dir, h->n_cu, (void*)d);
+    const int n = sgm::census_path_items(g, only_dir, h->n_cu, nullptr, 0);
+    if (h->items_key == key) return n;
+    if (n > l.n_items) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");          // a previous upload may still read the buffer
+    if (st != h->stream) HIP_TRY(hipStreamSynchronize(st), "sync");
+    if (n > h->items_cap) {
+        if (h->items_pin) (void)hipHostFree(h->items_pin);
+        h->items_pin = nullptr;
+        h->items_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&h->items_pin, (size_t)n * 4, hipHostMallocDefault), "hipHostMalloc");
+        h->items_cap = n;
+    }
+    sgm::census_path_items(g, only_dir, h->n_cu, h->items_pin, h->items_cap);
+    HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
+    h->items_key = key;
+    return n;
+}
+
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
                  int16_t* dOut, size_t out_stride)
@@ -261,8 +300,11 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         uint8_t* vols = (uint8_t*)(ws + l.vols);
         rec.begin("census", 2 * WH + 16 * WH);
         HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
+        const uint32_t* items;
+        const int n_items = path_items(h, l, g, -1, st, &items);
+        if (n_items < 0) return n_items;
         rec.begin("paths8", 8 * cells);
-        HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, -1, st), "paths");
+        HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
         HIP_TRY(sgm::launch_census_wta(vols, l.vol_bytes, g, dst, dst_stride, st), "wta");
     } else {
@@ -299,6 +341,8 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l)
     if (rc) return rc;
     if ((rc = ensure_stream(h))) return rc;
     l = make_layout(h->params, g, host_io);
+    // the uploaded path work list lives in the workspace: any other use of it invalidates it
+    if (h->params.mode != SGM_MODE_CENSUS8) h->items_key.clear();
     return ensure_ws(h, l.total);
 }
 
@@ -352,6 +396,7 @@ void sgm_destroy(sgm_handle* h)
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (h->ws.base) (void)hipFree(h->ws.base);
         if (h->pin) (void)hipHostFree(h->pin);
+        if (h->items_pin) (void)hipHostFree(h->items_pin);
         for (auto& r : h->prof)
             for (int i = 0; i <= SGM_MAX_STAGES; i++) (void)hipEventDestroy(r.ev[i]);
         if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -567,7 +612,10 @@ int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int
     uint8_t* vols = (uint8_t*)(ws + l.vols);
     HIP_TRY(sgm::launch_census((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, W, H, cL, cR, h->stream),
             "census");
-    HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, dir, h->stream), "paths");
+    const uint32_t* items;
+    const int n_items = path_items(h, l, g, dir, h->stream, &items);
+    if (n_items < 0) return n_items;
+    HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, items, n_items, h->stream), "paths");
     const size_t cells = (size_t)g.width1 * g.H * g.D;
     HIP_TRY(hipMemcpyAsync(vol, vols + (size_t)dir * l.vol_bytes, cells, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
