@@ -1,17 +1,53 @@
-"""Summarise rocprofv3 --pmc CSVs per kernel: mean counter value per dispatch."""
+"""Summarise rocprofv3 --pmc CSVs per kernel (mean counter value per dispatch).
+
+    python tools/pmc_summary.py gpurun_out/pmc [--config c3] [--out profiles/latest_pmc.json]
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE counts half the bytes of wide coalesced streaming reads, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores. The path kernel's reads
+are 8-B census codes (an uncalibrated width): its FETCH figure is indicative only.
+"""
+import argparse
 import collections
 import csv
 import glob
 import json
-import sys
 
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(f"{d}/pass*_counter_collection.csv")):
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-out = {}
-for k, cs in acc.items():
-    out[k] = {c: sum(v) / len(v) for c, v in cs.items()}
-json.dump(out, sys.stdout, indent=1)
+STAGE_OF = {"k_census9x7": "census", "k_census_paths16": "paths8", "k_census_wta16": "wta_lr",
+            "k_ocv_pixcost": "ocv_cost", "k_ocv_paths": "ocv_paths", "k_ocv_wta": "ocv_wta_lr"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(f"{args.dir}/pass*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    raw = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+    kernels = {}
+    for k, cs in raw.items():
+        base = k.split("<")[0].replace("sgm::", "")
+        stage = STAGE_OF.get(base)
+        if stage is None or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        fetch = 2.0 * cs["FETCH_SIZE"] * 1024.0
+        write = cs["WRITE_SIZE"] * 1024.0
+        kernels[stage] = {"kernel": k, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                          "hbm_bytes_per_launch": fetch + write,
+                          "valu_insts": cs.get("SQ_INSTS_VALU"), "salu_insts": cs.get("SQ_INSTS_SALU"),
+                          "lds_insts": cs.get("SQ_INSTS_LDS")}
+    out = {"config": args.config, "source": "rocprofv3 --pmc (tools/pmc.sh), mean per dispatch",
+           "kernels": kernels, "raw": raw}
+    s = json.dumps(out, indent=1)
+    if args.out:
+        open(args.out, "w").write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
