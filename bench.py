@@ -39,6 +39,16 @@ def shard_frames(n_frames_per_rank, rank, seed0=0):
     return [seed0 + rank * n_frames_per_rank + i for i in range(n_frames_per_rank)]
 
 
+def max_over_ranks(x, device=None):
+    """MAX of a float over all ranks (the timing reduction; RCCL on GPUs, gloo in tests)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def algorithmic_bytes(w, h, D, width1):
     """SURVEY §8d B_alg per stereo pair, evaluated on the aggregated cells (width1 x H x D):
     2 B/px images in + 8 u8 path volumes written + read once (16 B/cell) + 2 B/px out."""
@@ -165,10 +175,7 @@ def main():
     n_prof = eng.profiled_matches()
     eng.set_profiling(False)
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    elapsed_max = max_over_ranks(elapsed, device)
 
     frames_total = args.frames * args.steps * world
     value = frames_total / elapsed_max
