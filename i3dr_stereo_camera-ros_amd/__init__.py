@@ -38,9 +38,10 @@ MISSING_Z = 10000.0  # image_geometry::StereoCameraModel::MISSING_Z
 
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
-    "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_batch", "sgm_synchronize", "sgm_last_error",
+    "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch",
+    "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
-    "sgm_debug_census",
+    "sgm_stage_launches", "sgm_debug_census",
     "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
 ]
 
@@ -95,6 +96,7 @@ def load_library(path=LIB_PATH):
     L.sgm_check_params.argtypes = [P(SgmParams), ci, ci]
     L.sgm_match.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz]
     L.sgm_match_device.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, vp]
+    L.sgm_match_device_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, vp]
     L.sgm_match_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, P(ci), ci]
     L.sgm_synchronize.argtypes = [vp]
     L.sgm_last_error.argtypes = [vp]
@@ -105,6 +107,7 @@ def load_library(path=LIB_PATH):
     L.sgm_stage_name.argtypes = [vp, ci]
     L.sgm_stage_name.restype = ctypes.c_char_p
     L.sgm_stage_bytes.argtypes = [vp, ci]
+    L.sgm_stage_launches.argtypes = [vp, ci]
     L.sgm_stage_bytes.restype = ctypes.c_double
     L.sgm_debug_census.argtypes = [vp, vp, ci, ci, sz, vp]
     L.sgm_debug_census_path.argtypes = [vp, vp, vp, ci, ci, sz, ci, vp]
@@ -203,6 +206,15 @@ class Engine:
                                               height, stride, ctypes.c_void_p(d_out), out_stride,
                                               ctypes.c_void_p(stream) if stream else None))
 
+    def match_device_batch(self, d_lefts, d_rights, width, height, stride, d_outs, out_stride, stream=None):
+        """Frame batch of device pointers; census mode pipelines consecutive frames (the
+        aggregation of frame i+1 shares one launch with the WTA of frame i)."""
+        n = len(d_lefts)
+        arr = ctypes.c_void_p * max(n, 1)
+        self._check(self.lib.sgm_match_device_batch(self.h, arr(*d_lefts), arr(*d_rights), n, width, height, stride,
+                                                    arr(*d_outs), out_stride,
+                                                    ctypes.c_void_p(stream) if stream else None))
+
     def synchronize(self):
         self._check(self.lib.sgm_synchronize(self.h))
 
@@ -231,8 +243,13 @@ class Engine:
     def profiled_matches(self):
         return int(self.lib.sgm_profiled_matches(self.h))
 
+    def stage_launches(self):
+        """{stage: number of launches recorded since profiling was enabled}"""
+        return {self.lib.sgm_stage_name(self.h, i).decode(): int(self.lib.sgm_stage_launches(self.h, i))
+                for i in range(len(self.stage_times()))}
+
     def stage_times(self):
-        """[(stage, average ms over the profiled matches, algorithmic bytes per match)]"""
+        """[(stage, average ms per launch, algorithmic bytes per launch)], first-launch order"""
         buf = (ctypes.c_float * 16)()
         n = self.lib.sgm_get_stage_times(self.h, buf, 16)
         if n < 0:

@@ -282,15 +282,18 @@ __device__ __forceinline__ void seg_load(uint64_t (&v)[RowSeg<DPL>::NLOAD], cons
     using RS = RowSeg<DPL>;
     const int y = ry > 0 ? s : g.H - 1 - s;
     const int yc = min(max(y, 0), g.H - 1);
-    const uint64_t* cLr = cL + (size_t)yc * g.W;
-    const uint64_t* cRr = cR + (size_t)yc * g.W;
+    // one wave-uniform base for both code images + 32-bit element offsets
+    // (SGPR-base + VGPR-offset loads instead of per-lane 64-bit address arithmetic)
+    const uint64_t* base = cL < cR ? cL : cR;
+    const uint32_t oL = (uint32_t)(cL - base) + (uint32_t)(yc * g.W);
+    const uint32_t oR = (uint32_t)(cR - base) + (uint32_t)(yc * g.W);
     const int xs = xb + rx * s;
     const int seg0 = xs - g.minD - 16 * DPL + 1;
 #pragma unroll
     for (int m = 0; m < RS::NLOAD; m++) {
         const int q = min(tid + m * kWG, RS::NTOT - 1);
         const int idx = q < RS::NSEG ? seg0 + q : xs + (q - RS::NSEG);
-        v[m] = (q < RS::NSEG ? cRr : cLr)[min(max(idx, 0), g.W - 1)];
+        v[m] = base[(q < RS::NSEG ? oR : oL) + (uint32_t)min(max(idx, 0), g.W - 1)];
     }
 }
 
@@ -331,7 +334,8 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     for (int i = 0; i < M; i++) Lr[i] = start[i];
     bool pv = false;
     const bool lane_act = EXACT || p * DPL < g.D;
-    uint8_t* tr = trash + (tid & 63) * DPL;
+    // stores: 32-bit offsets from the wave-uniform volume base (cells or the trash slot)
+    const uint32_t tr_off = (uint32_t)(trash - V) + (uint32_t)((tid & 63) * DPL);
     const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
 
     uint64_t* buf0 = lds;
@@ -348,12 +352,13 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         const int y = ry > 0 ? s : g.H - 1 - s;
         const uint64_t cl = bufc[RS::NPAD + j];
         uint32_t Labs[M];
-#pragma unroll
-        for (int i = 0; i < M; i++) Lr[i] = pv ? Lr[i] : start[i];      // path start: L = C
-        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2P2, imask, Labs);
-        uint8_t* dst = (valid && lane_act)
-            ? V + ((size_t)min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL : tr;
-        store_pairs<DPL>(dst, Labs);
+        // path start (first valid pixel of the line): L = C. The P2 cap of the recurrence is
+        // lowered to "0" (kBase), which clamps every candidate: one select per step.
+        const uint32_t P2x = pv ? P2P2 : kBaseP2;
+        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
+        const uint32_t off = (valid && lane_act)
+            ? (uint32_t)((min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL) : tr_off;
+        store_pairs<DPL>(V + off, Labs);
         pv = valid;
     };
     for (int s = s0; s < s1; s += 2) {
@@ -368,14 +373,12 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     }
 }
 
+// One work-list entry: 16 lines of one direction (lds: 2 * RowSeg<DPL>::BUF u64).
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restrict__ cL,
-                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
-                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                                                        const uint32_t* __restrict__ items)
+__device__ __forceinline__ void paths_block16(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
+                                              uint8_t* __restrict__ vols, size_t vol_bytes, size_t trash_off,
+                                              const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
-    __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
-    const uint32_t it = items[blockIdx.x];
     const int dir = (int)(it >> 24);
     const int lb = (int)(it & 0xFFFFFFu);
     uint8_t* V = vols + (size_t)dir * vol_bytes;
@@ -383,6 +386,16 @@ __global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restri
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
+}
+
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restrict__ cL,
+                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
+                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
+                                                        const uint32_t* __restrict__ items)
+{
+    __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
+    paths_block16<DPL, EXACT>(cL, cR, vols, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
 }
 
 // ====================================================================================
@@ -398,14 +411,6 @@ __global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restri
 // Results go to the row's LDS arrays; row_finish() does disp2 (LDS atomics) + LR + store.
 // ====================================================================================
 template <int DPL>
-struct WVec;
-template <> struct WVec<2> { using T = uint16_t; static constexpr int NW = 1; };
-template <> struct WVec<4> { using T = uint32_t; static constexpr int NW = 1; };
-template <> struct WVec<8> { using T = uint2; static constexpr int NW = 2; };
-template <> struct WVec<16> { using T = uint4; static constexpr int NW = 4; };
-template <> struct WVec<32> { using T = uint4; static constexpr int NW = 4; };   // two vectors
-
-template <int DPL>
 __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 3) / 4])
 {
     if constexpr (DPL == 2) { wd[0] = *(const uint16_t*)src; }
@@ -420,27 +425,31 @@ __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 
     }
 }
 
+// LDS bytes of one WTA row (per-row S slices + RowLds)
+template <int DPL>
+__host__ __device__ constexpr size_t wta_lds_bytes(int W) { return (size_t)kWG * DPL * 2 + RowLds::bytes(W); }
+
+// One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
-                                                      int16_t* __restrict__ out, size_t out_stride)
+__device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size_t vol_bytes, const Geom& g,
+                                          int16_t* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
 {
     constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
-    extern __shared__ uint32_t lds_wta[];
-    uint32_t* sl = lds_wta;                       // 4 waves x 4 rows x 16*DPL u16 S values
-    RowLds R(lds_wta + kWG * DPL / 2, g.W);
+    uint32_t* sl = lds;                           // 4 waves x 4 rows x 16*DPL u16 S values
+    RowLds R(lds + kWG * DPL / 2, g.W);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane >> 4, p = lane & 15;
-    const int y = blockIdx.x;
     R.init(g, tid, kWG);
     const bool lane_act = EXACT || p * DPL < g.D;
-    const uint8_t* vrow = vols + (size_t)y * g.width1 * g.D + (lane_act ? p * DPL : 0);
+    // 32-bit offsets from wave-uniform volume bases: SGPR-base + VGPR-offset addressing
+    const uint32_t off0 = (uint32_t)(y * g.width1 * g.D) + (lane_act ? p * DPL : 0);
     uint32_t* srow = sl + (w * 4 + r) * 8 * DPL;
     const int n = g.width1;
     const int nq = (n + 3) / 4;
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
-        const int x1 = min(4 * q + r, n - 1);
+        const uint32_t off = off0 + (uint32_t)(min(4 * q + r, n - 1) * g.D);
 #pragma unroll
-        for (int vv = 0; vv < 8; vv++) wload<DPL>(vrow + (size_t)vv * vol_bytes + (size_t)x1 * g.D, v[vv]);
+        for (int vv = 0; vv < 8; vv++) wload<DPL>(vols + (size_t)vv * vol_bytes + off, v[vv]);
     };
     uint32_t cur[8][NWD], nxt[8][NWD];
     load(min(w, nq - 1), cur);
@@ -509,6 +518,36 @@ __global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict_
             for (int j = 0; j < NWD; j++) cur[vv][j] = nxt[vv][j];
     }
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+}
+
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
+                                                      int16_t* __restrict__ out, size_t out_stride)
+{
+    extern __shared__ uint32_t lds_dyn[];
+    wta_row16<DPL, EXACT>(vols, vol_bytes, g, out, out_stride, blockIdx.x, lds_dyn);
+}
+
+// ------------------------------------------------------------------------------------
+// Frame pipelining: one launch runs the path sweeps of frame i+1 (VALU-bound) and the WTA
+// rows of frame i (HBM-bound). Blocks [wta_at, wta_at + H) are WTA rows, the others walk
+// the path work list.
+// ------------------------------------------------------------------------------------
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_fused16(const uint64_t* __restrict__ cL,
+                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols_p,
+                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
+                                                        const uint32_t* __restrict__ items, int n_items,
+                                                        const uint8_t* __restrict__ vols_w, int16_t* __restrict__ out,
+                                                        size_t out_stride, int wta_at)
+{
+    extern __shared__ uint64_t lds_dyn64[];
+    const int b = blockIdx.x;
+    if (b >= wta_at && b < wta_at + g.H)
+        wta_row16<DPL, EXACT>(vols_w, vol_bytes, g, out, out_stride, b - wta_at, (uint32_t*)lds_dyn64);
+    else
+        paths_block16<DPL, EXACT>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items[b < wta_at ? b : b - g.H],
+                                  lds_dyn64);
 }
 
 // ------------------------------------------------------------------------------------
@@ -610,7 +649,7 @@ static void launch_wta_dpl(const uint8_t* vols, size_t vol_bytes, const Geom& g,
                            hipStream_t st)
 {
     dim3 grid(g.H), block(kWG);
-    const size_t lds = (size_t)kWG * DPL * 2 + RowLds::bytes(g.W);
+    const size_t lds = wta_lds_bytes<DPL>(g.W);
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, vols, vol_bytes, g, out, out_stride);
     else
@@ -626,6 +665,42 @@ hipError_t launch_census_wta(const uint8_t* vols, size_t vol_bytes, const Geom& 
     case 8: launch_wta_dpl<8>(vols, vol_bytes, g, out, out_stride, st); break;
     case 16: launch_wta_dpl<16>(vols, vol_bytes, g, out, out_stride, st); break;
     default: launch_wta_dpl<32>(vols, vol_bytes, g, out, out_stride, st); break;
+    }
+    return hipGetLastError();
+}
+
+template <int DPL>
+static void launch_fused_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vols_p, size_t vol_bytes,
+                             size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
+                             int n_items, const uint8_t* vols_w, int16_t* out, size_t out_stride, hipStream_t st)
+{
+    dim3 grid(n_items + g.H), block(kWG);
+    const size_t lds = std::max(wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF);
+    // WTA rows after all path blocks: they fill the CUs the path sweeps' tail leaves idle
+    // (measured at C3: WTA first 2.02 ms, interleaved 1.97, evenly from 30 % 1.92, last 1.71)
+    const int wta_at = n_items;
+    if (g.D == 16 * DPL)
+        hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, cL, cR, vols_p, vol_bytes, trash_off,
+                           g, pl, items, n_items, vols_w, out, out_stride, wta_at);
+    else
+        hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, cL, cR, vols_p, vol_bytes, trash_off,
+                           g, pl, items, n_items, vols_w, out, out_stride, wta_at);
+}
+
+// Paths of one frame (codes cL/cR -> volumes vols_p) fused with the WTA of the previous
+// frame (volumes vols_w -> out). Both volume sets have the same geometry.
+hipError_t launch_census_fused(const uint64_t* cL, const uint64_t* cR, uint8_t* vols_p, size_t vol_bytes,
+                               const Geom& g, const uint32_t* items, int n_items, const uint8_t* vols_w,
+                               int16_t* out, size_t out_stride, hipStream_t st)
+{
+    const PathLaunch16 pl = make_path_launch16(g);
+    const size_t trash_off = (size_t)g.H * g.width1 * g.D;
+    switch (dpl16_for(g.D)) {
+    case 2: launch_fused_dpl<2>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
+    case 4: launch_fused_dpl<4>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
+    case 8: launch_fused_dpl<8>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
+    case 16: launch_fused_dpl<16>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
+    default: launch_fused_dpl<32>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
     }
     return hipGetLastError();
 }

@@ -25,6 +25,8 @@ int census_path_items(const Geom&, int, int, uint32_t*, int);
 hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, const uint32_t*, int,
                                hipStream_t);
 hipError_t launch_census_wta(const uint8_t*, size_t, const Geom&, int16_t*, size_t, hipStream_t);
+hipError_t launch_census_fused(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, const uint32_t*, int,
+                               const uint8_t*, int16_t*, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -99,11 +101,15 @@ struct sgm_handle {
     Workspace ws;
     uint8_t* pin = nullptr;      // pinned host staging
     size_t pin_size = 0;
+    // profiling: one hipEvent before every launch and one after the last launch of a
+    // match; launch k runs from event `start` to the next recorded event
     bool profiling = false;
-    struct ProfRec { hipEvent_t ev[SGM_MAX_STAGES + 1]; int n; };
-    std::vector<ProfRec> prof;     // event pool, one record per profiled match
-    size_t prof_used = 0;
-    int nstages = 0;
+    std::vector<hipEvent_t> ev_pool;   // grows on demand, reused after a re-enable
+    size_t ev_used = 0;
+    struct LaunchRec { int stage; size_t ev0, ev1; };
+    std::vector<LaunchRec> launches;
+    int prof_frames = 0;
+    int nstages = 0;                   // distinct stage names seen (first-launch order)
     const char* stage_name[SGM_MAX_STAGES] = {};
     double stage_bytes[SGM_MAX_STAGES] = {};
     std::vector<sgm_handle*> sub;  // per-device handles for sgm_match_batch
@@ -140,20 +146,26 @@ int ensure_stream(sgm_handle* h)
     return SGM_OK;
 }
 
-// Next free event record of the profiling pool (grows on demand; events are reused after a
-// re-enable). Returns nullptr when profiling is off.
-sgm_handle::ProfRec* next_prof(sgm_handle* h)
+// Records the next pool event on the handle's stream; returns its index or -1.
+long record_event(sgm_handle* h)
 {
-    if (!h->profiling) return nullptr;
-    if (h->prof_used == h->prof.size()) {
-        sgm_handle::ProfRec r{};
-        for (int i = 0; i <= SGM_MAX_STAGES; i++)
-            if (hipEventCreate(&r.ev[i]) != hipSuccess) return nullptr;
-        h->prof.push_back(r);
+    if (h->ev_used == h->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        h->ev_pool.push_back(e);
     }
-    sgm_handle::ProfRec* r = &h->prof[h->prof_used++];
-    r->n = 0;
-    return r;
+    if (hipEventRecord(h->ev_pool[h->ev_used], h->stream) != hipSuccess) return -1;
+    return (long)h->ev_used++;
+}
+
+int stage_index(sgm_handle* h, const char* name, double bytes)
+{
+    for (int i = 0; i < h->nstages; i++)
+        if (std::strcmp(h->stage_name[i], name) == 0) { h->stage_bytes[i] = bytes; return i; }
+    if (h->nstages == SGM_MAX_STAGES) return -1;
+    h->stage_name[h->nstages] = name;
+    h->stage_bytes[h->nstages] = bytes;
+    return h->nstages++;
 }
 
 int ensure_ws(sgm_handle* h, size_t bytes)
@@ -189,13 +201,14 @@ int ensure_pin(sgm_handle* h, size_t bytes)
 struct Layout {
     size_t cL = 0, cR = 0, vols = 0, vol_bytes = 0;       // census
     size_t items = 0; int n_items = 0;                     // census path work list
+    size_t cL2 = 0, cR2 = 0, vols2 = 0;                    // census: second set (pipelined batch)
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovol_elems = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0;                      // host-API staging
     size_t total = 0;
 };
 
-Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
+Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, bool two_sets = false)
 {
     Layout l;
     size_t off = 0;
@@ -211,6 +224,11 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
             l.n_items = sgm::census_path_items(g, -1, 1, nullptr, 0);
             l.items = take((size_t)l.n_items * 4);
         }
+        if (two_sets) {
+            l.cL2 = take(WH * 8);
+            l.cR2 = take(WH * 8);
+            l.vols2 = take(l.vol_bytes * 8);
+        }
     } else {
         l.planes = take(WH * 4);
         l.bufA = take(cells * 2);
@@ -225,26 +243,28 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io)
     return l;
 }
 
+// Stage bookkeeping of one match call: begin() before every launch, end() after the last.
 struct StageRec {
     sgm_handle* h;
-    sgm_handle::ProfRec* r = nullptr;
-    int n = 0;
+    long open = -1;      // index into h->launches of the launch waiting for its end event
+    void close(long ev)
+    {
+        if (open >= 0 && ev >= 0) h->launches[open].ev1 = (size_t)ev;
+        open = -1;
+    }
     void begin(const char* name, double bytes)
     {
-        if (n < SGM_MAX_STAGES) {
-            h->stage_name[n] = name;
-            h->stage_bytes[n] = bytes;
-            if (r) (void)hipEventRecord(r->ev[n], h->stream);
-        }
-        n++;
+        const int st = stage_index(h, name, bytes);
+        if (!h->profiling) return;
+        const long ev = record_event(h);
+        close(ev);
+        if (st < 0 || ev < 0) return;
+        h->launches.push_back({st, (size_t)ev, (size_t)ev});
+        open = (long)h->launches.size() - 1;
     }
     void end()
     {
-        h->nstages = std::min(n, SGM_MAX_STAGES);
-        if (r) {
-            (void)hipEventRecord(r->ev[h->nstages], h->stream);
-            r->n = h->nstages;
-        }
+        if (h->profiling && open >= 0) close(record_event(h));
     }
 };
 
@@ -259,8 +279,6 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, hipS
     const int n = sgm::census_path_items(g, only_dir, h->n_cu, nullptr, 0);
     if (h->items_key == key) return n;
     if (n > l.n_items) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
-    HIP_TRY(hipStreamSynchronize(h->stream), "sync");          // a previous upload may still read the buffer
-    if (st != h->stream) HIP_TRY(hipStreamSynchronize(st), "sync");
     if (n > h->items_cap) {
         if (h->items_pin) (void)hipHostFree(h->items_pin);
         h->items_pin = nullptr;
@@ -270,8 +288,28 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, hipS
     }
     sgm::census_path_items(g, only_dir, h->n_cu, h->items_pin, h->items_cap);
     HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
+    HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
     h->items_key = key;
     return n;
+}
+
+// Post filters of one finished frame (src = the WTA output in `tmp` when a median runs).
+int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_t out_stride, StageRec& rec)
+{
+    const sgm_params& p = h->params;
+    char* ws = (char*)h->ws.base;
+    const double WH = (double)g.W * g.H;
+    if (use_median(p)) {
+        rec.begin("median3", 4 * WH);
+        HIP_TRY(sgm::launch_median3((int16_t*)(ws + l.tmp), g.W, dOut, out_stride, g.W, g.H, h->stream), "median3");
+    }
+    if (p.speckle_window_size > 0) {
+        rec.begin("speckle", 14 * WH);
+        HIP_TRY(sgm::launch_speckle(dOut, out_stride, g.W, g.H, g.invalid, p.speckle_window_size,
+                                    16 * p.speckle_range, (int*)(ws + l.lab), (int*)(ws + l.cnt), h->stream),
+                "speckle");
+    }
+    return SGM_OK;
 }
 
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
@@ -282,15 +320,14 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
     char* ws = (char*)h->ws.base;
     hipStream_t st = h->stream;
     const bool med = use_median(p);
-    const bool spk = p.speckle_window_size > 0;
     int16_t* tmp = (int16_t*)(ws + l.tmp);
     // the disparity producer writes to `tmp` when a median follows, else directly to dOut
     int16_t* dst = med ? tmp : dOut;
     const size_t dst_stride = med ? (size_t)g.W : out_stride;
     const double WH = (double)g.W * g.H;
     const double cells = (double)std::max(g.width1, 0) * g.H * g.D;
-    StageRec rec{h, next_prof(h)};
-    h->nstages = 0;
+    StageRec rec{h};
+    if (h->profiling) h->prof_frames++;
     if (g.width1 <= 0) {
         rec.begin("fill_invalid", 2 * WH);
         HIP_TRY(sgm::launch_fill16(dst, dst_stride, g.W, g.H, g.invalid, st), "fill");
@@ -321,26 +358,70 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("ocv_wta_lr", 2 * cells * ndir + 2 * WH);
         HIP_TRY(sgm::launch_ocv_wta(V, l.ovol_elems, ndir, g, dst, dst_stride, st), "ocv_wta");
     }
-    if (med) {
-        rec.begin("median3", 4 * WH);
-        HIP_TRY(sgm::launch_median3(tmp, g.W, dOut, out_stride, g.W, g.H, st), "median3");
-    }
-    if (spk) {
-        rec.begin("speckle", 14 * WH);
-        HIP_TRY(sgm::launch_speckle(dOut, out_stride, g.W, g.H, g.invalid, p.speckle_window_size,
-                                    16 * p.speckle_range, (int*)(ws + l.lab), (int*)(ws + l.cnt), st),
-                "speckle");
+    int rc = run_post(h, l, g, dOut, out_stride, rec);
+    if (rc) return rc;
+    rec.end();
+    return SGM_OK;
+}
+
+// Census-mode frame pipeline over n >= 2 frames on h->stream (two workspace sets):
+//   census(0) paths(0) | census(i) fused[paths(i) + wta(i-1)] post(i-1) ... | wta(n-1) post(n-1)
+int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* const* dLs,
+                     const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride)
+{
+    const sgm_params& p = h->params;
+    char* ws = (char*)h->ws.base;
+    hipStream_t st = h->stream;
+    const bool med = use_median(p);
+    const double WH = (double)g.W * g.H;
+    const double cells = (double)g.width1 * g.H * g.D;
+    uint64_t* cL[2] = {(uint64_t*)(ws + l.cL), (uint64_t*)(ws + l.cL2)};
+    uint64_t* cR[2] = {(uint64_t*)(ws + l.cR), (uint64_t*)(ws + l.cR2)};
+    uint8_t* vols[2] = {(uint8_t*)(ws + l.vols), (uint8_t*)(ws + l.vols2)};
+    int16_t* tmp = (int16_t*)(ws + l.tmp);
+    const uint32_t* items;
+    const int n_items = path_items(h, l, g, -1, st, &items);
+    if (n_items < 0) return n_items;
+    StageRec rec{h};
+    if (h->profiling) h->prof_frames += n;
+    for (int i = 0; i <= n; i++) {
+        const int s = i & 1;
+        if (i < n) {
+            rec.begin("census", 2 * WH + 16 * WH);
+            HIP_TRY(sgm::launch_census(dLs[i], dRs[i], stride, g.W, g.H, cL[s], cR[s], st), "census");
+        }
+        int16_t* dst = nullptr;
+        size_t dst_stride = 0;
+        if (i > 0) {
+            dst = med ? tmp : outs[i - 1];
+            dst_stride = med ? (size_t)g.W : out_stride;
+        }
+        if (i == 0) {
+            rec.begin("paths8", 8 * cells);
+            HIP_TRY(sgm::launch_census_paths(cL[s], cR[s], vols[s], l.vol_bytes, g, items, n_items, st), "paths");
+        } else if (i < n) {
+            rec.begin("paths8+wta_lr", 16 * cells + 2 * WH);
+            HIP_TRY(sgm::launch_census_fused(cL[s], cR[s], vols[s], l.vol_bytes, g, items, n_items, vols[s ^ 1], dst,
+                                             dst_stride, st), "fused");
+        } else {
+            rec.begin("wta_lr", 8 * cells + 2 * WH);
+            HIP_TRY(sgm::launch_census_wta(vols[s ^ 1], l.vol_bytes, g, dst, dst_stride, st), "wta");
+        }
+        if (i > 0) {
+            int rc = run_post(h, l, g, outs[i - 1], out_stride, rec);
+            if (rc) return rc;
+        }
     }
     rec.end();
     return SGM_OK;
 }
 
-int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l)
+int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, bool two_sets = false)
 {
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
     if ((rc = ensure_stream(h))) return rc;
-    l = make_layout(h->params, g, host_io);
+    l = make_layout(h->params, g, host_io, two_sets);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
     if (h->params.mode != SGM_MODE_CENSUS8) h->items_key.clear();
     return ensure_ws(h, l.total);
@@ -397,8 +478,7 @@ void sgm_destroy(sgm_handle* h)
         if (h->ws.base) (void)hipFree(h->ws.base);
         if (h->pin) (void)hipHostFree(h->pin);
         if (h->items_pin) (void)hipHostFree(h->items_pin);
-        for (auto& r : h->prof)
-            for (int i = 0; i <= SGM_MAX_STAGES; i++) (void)hipEventDestroy(r.ev[i]);
+        for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -442,6 +522,34 @@ int sgm_match_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W,
     hipStream_t own = h->stream;
     if (stream) h->stream = (hipStream_t)stream;
     rc = run_pipeline(h, l, g, dL, dR, stride, dOut, out_stride);
+    h->stream = own;
+    return rc;
+}
+
+int sgm_match_device_batch(sgm_handle* h, const uint8_t* const* dLs, const uint8_t* const* dRs, int n, int W, int H,
+                           size_t stride, int16_t* const* outs, size_t out_stride, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (n < 0 || (n > 0 && (!dLs || !dRs || !outs)) || stride < (size_t)W || out_stride < (size_t)W)
+        return fail(h, SGM_ERR_ARG, "bad buffers");
+    for (int i = 0; i < n; i++)
+        if (!dLs[i] || !dRs[i] || !outs[i]) return fail(h, SGM_ERR_ARG, "null frame pointer");
+    if (n == 0) return SGM_OK;
+    Geom g;
+    Layout l;
+    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2;
+    int rc = make_geom(h->params, W, H, g, h->err);
+    if (rc) return rc;
+    rc = prepare(h, W, H, false, g, l, pipelined && g.width1 > 0);
+    if (rc) return rc;
+    hipStream_t own = h->stream;
+    if (stream) h->stream = (hipStream_t)stream;
+    if (pipelined && g.width1 > 0) {
+        rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride);
+    } else {
+        for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
+    }
     h->stream = own;
     return rc;
 }
@@ -532,34 +640,33 @@ int sgm_set_profiling(sgm_handle* h, int enable)
     std::lock_guard<std::mutex> lk(h->mu);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->profiling = enable != 0;
-    h->prof_used = 0;
+    h->ev_used = 0;
+    h->launches.clear();
+    h->prof_frames = 0;
+    h->nstages = 0;
     return SGM_OK;
 }
 
-int sgm_profiled_matches(const sgm_handle* h) { return h ? (int)h->prof_used : 0; }
+int sgm_profiled_matches(const sgm_handle* h) { return h ? h->prof_frames : 0; }
 
 int sgm_get_stage_times(sgm_handle* h, float* ms, int max)
 {
     if (!h || !ms) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->prof_used == 0) return 0;
+    if (h->launches.empty()) return 0;
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-    const sgm_handle::ProfRec& last = h->prof[h->prof_used - 1];
-    HIP_TRY(hipEventSynchronize(last.ev[last.n]), "hipEventSynchronize");
-    const int n = std::min(last.n, max);
-    std::vector<double> acc(n, 0.0);
-    int cnt = 0;
-    for (size_t k = 0; k < h->prof_used; k++) {
-        const sgm_handle::ProfRec& r = h->prof[k];
-        if (r.n != last.n) continue;
-        for (int i = 0; i < n; i++) {
-            float t = 0.f;
-            HIP_TRY(hipEventElapsedTime(&t, r.ev[i], r.ev[i + 1]), "hipEventElapsedTime");
-            acc[i] += t;
-        }
-        cnt++;
+    HIP_TRY(hipEventSynchronize(h->ev_pool[h->ev_used - 1]), "hipEventSynchronize");
+    const int n = std::min(h->nstages, max);
+    std::vector<double> acc(h->nstages, 0.0);
+    std::vector<int> cnt(h->nstages, 0);
+    for (const auto& r : h->launches) {
+        if (r.ev1 == r.ev0) continue;           // never closed
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, h->ev_pool[r.ev0], h->ev_pool[r.ev1]), "hipEventElapsedTime");
+        acc[r.stage] += t;
+        cnt[r.stage]++;
     }
-    for (int i = 0; i < n; i++) ms[i] = (float)(acc[i] / std::max(cnt, 1));
+    for (int i = 0; i < n; i++) ms[i] = (float)(acc[i] / std::max(cnt[i], 1));
     return n;
 }
 
@@ -573,6 +680,14 @@ double sgm_stage_bytes(const sgm_handle* h, int i)
 {
     if (!h || i < 0 || i >= h->nstages) return 0.0;
     return h->stage_bytes[i];
+}
+
+int sgm_stage_launches(const sgm_handle* h, int i)
+{
+    if (!h || i < 0 || i >= h->nstages) return 0;
+    int c = 0;
+    for (const auto& r : h->launches) c += (r.stage == i && r.ev1 != r.ev0) ? 1 : 0;
+    return c;
 }
 
 // ------------------------------------------------------------------ stage entry points

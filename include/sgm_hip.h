@@ -114,6 +114,14 @@ int  sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* 
                      int16_t* const* disps, size_t out_stride,
                      const int* devices, int n_dev);
 
+/* Frame batch on device buffers (host arrays of n_frames device pointers), asynchronous on
+ * `stream`. Census mode pipelines the frames: the path aggregation of frame i+1 and the
+ * WTA of frame i run in ONE launch (VALU-bound and HBM-bound work side by side), with two
+ * workspace volume sets. Results are identical to n_frames sgm_match_device calls.     */
+int  sgm_match_device_batch(sgm_handle* h, const uint8_t* const* d_lefts, const uint8_t* const* d_rights,
+                            int n_frames, int width, int height, size_t stride,
+                            int16_t* const* d_disps, size_t out_stride, void* stream);
+
 /* Synchronise the handle's stream (after sgm_match_device with stream == NULL).          */
 int  sgm_synchronize(sgm_handle* h);
 
@@ -121,17 +129,19 @@ const char* sgm_last_error(const sgm_handle* h);
 
 /* ---- profiling: per-stage device time (hipEvents on the handle's stream) ---------------- */
 #define SGM_MAX_STAGES 16
-/* enable != 0: (re)start recording a hipEvent before/after every stage of every match;
- * the records of all matches since the last enable are kept (no host sync per match).     */
+/* enable != 0: (re)start recording a hipEvent around every kernel launch ("stage") of
+ * every match; records since the last enable are kept (no host sync per match).          */
 int  sgm_set_profiling(sgm_handle* h, int enable);
-/* Synchronises on the last record, fills up to `max` per-stage AVERAGE times (ms) over the
- * recorded matches of the current geometry; returns the number of stages.                */
+/* Synchronises on the last record and fills up to `max` per-stage AVERAGE times (ms per
+ * launch) — stages are identified by name, in first-launch order; returns their number. */
 int  sgm_get_stage_times(sgm_handle* h, float* ms, int max);
-/* Number of matches averaged by sgm_get_stage_times.                                      */
+/* Number of frames matched while profiling.                                               */
 int  sgm_profiled_matches(const sgm_handle* h);
 const char* sgm_stage_name(const sgm_handle* h, int i);
-/* Algorithmic HBM bytes of stage i for the last match geometry. */
+/* Algorithmic HBM bytes per launch of stage i.                         */
 double sgm_stage_bytes(const sgm_handle* h, int i);
+/* Number of launches of stage i recorded since profiling was enabled.                    */
+int  sgm_stage_launches(const sgm_handle* h, int i);
 
 /* ---- stage entry points (parity tests compare each stage with the CPU oracle) ----------- */
 /* 9x7 census codes of one image (host buffers; out: W x H uint64, row-major).             */

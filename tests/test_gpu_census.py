@@ -179,3 +179,36 @@ def test_profiling_stage_times(engine, pkg, synth):
     names = [s[0] for s in st]
     assert names[:3] == ["census", "paths8", "wta_lr"]
     assert all(t >= 0 for _, t, _ in st) and all(b > 0 for _, _, b in st)
+
+
+@pytest.mark.parametrize("kw,n", [(dict(num_disparities=64), 2), (dict(num_disparities=48, min_disparity=3), 3),
+                                  (dict(num_disparities=128, median=1, speckle_window_size=20, speckle_range=2), 4),
+                                  (dict(num_disparities=256), 5), (dict(num_disparities=32), 1)])
+def test_device_batch_pipeline(engine, oracle, pkg, synth, kw, n):
+    """sgm_match_device_batch (paths of frame i+1 fused with the WTA of frame i) returns
+    exactly the per-frame results, for every frame of the batch."""
+    torch = pytest.importorskip("torch")
+    D, minD = kw["num_disparities"], kw.get("min_disparity", 0)
+    h, w = 45, max(D + minD, 0) + 150
+    p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
+    engine.set_params(p)
+    frames = [synth.stereo_pair(h, w, max(minD, 0), D, seed=300 + 7 * i + D) for i in range(n)]
+    dl = [torch.from_numpy(f[0]).cuda() for f in frames]
+    dr = [torch.from_numpy(f[1]).cuda() for f in frames]
+    out = torch.full((n, h, w), 777, dtype=torch.int16, device="cuda")
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    engine.set_profiling(True)
+    engine.match_device_batch([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], w, h, w,
+                              [out[i].data_ptr() for i in range(n)], w, stream.cuda_stream)
+    stream.synchronize()
+    launches = engine.stage_launches()
+    engine.set_profiling(False)
+    got = out.cpu().numpy()
+    op = to_oracle_params(oracle, p)
+    for i, (l, r, _) in enumerate(frames):
+        ref = oracle.match(op, l, r)
+        assert np.array_equal(got[i], ref), f"frame {i}: {(got[i] != ref).sum()} pixels differ"
+    assert launches["census"] == n
+    if n >= 2:
+        assert launches["paths8"] == 1 and launches["paths8+wta_lr"] == n - 1 and launches["wta_lr"] == 1
