@@ -12,6 +12,8 @@
 #include "sgm_device.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace sgm {
@@ -69,8 +71,10 @@ __global__ __launch_bounds__(256) void k_census9x7(const uint8_t* __restrict__ L
 // So loops issue a fixed sequence: clamped prefetches, and cells that must not be written
 // (outside the image, d >= D, padding steps) go to a per-volume trash slot.
 // ====================================================================================
+// dst_hi: where bytes 16..31 go when DPL == 32 (D not a multiple of 32 leaves the lane that
+// straddles D half valid: its upper half must go to the trash slot, not the next pixel)
 template <int DPL>
-__device__ __forceinline__ void store_pairs(uint8_t* dst, const uint32_t (&L)[DPL / 2])
+__device__ __forceinline__ void store_pairs(uint8_t* dst, uint8_t* dst_hi, const uint32_t (&L)[DPL / 2])
 {
     // (lo, hi) u16 pairs with values <= 255 -> DPL consecutive bytes
     if constexpr (DPL == 2) {
@@ -83,7 +87,7 @@ __device__ __forceinline__ void store_pairs(uint8_t* dst, const uint32_t (&L)[DP
     } else {
 #pragma unroll
         for (int q = 0; q < DPL / 16; q++)
-            ((uint4*)dst)[q] = make_uint4(__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
+            *(uint4*)(q == 0 ? dst : dst_hi) = make_uint4(__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
                                           __builtin_amdgcn_perm(L[8 * q + 3], L[8 * q + 2], 0x06040200u),
                                           __builtin_amdgcn_perm(L[8 * q + 5], L[8 * q + 4], 0x06040200u),
                                           __builtin_amdgcn_perm(L[8 * q + 7], L[8 * q + 6], 0x06040200u));
@@ -233,6 +237,7 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     uint8_t* rowbase = V + (size_t)yc * g.width1 * g.D + p * DPL;
     uint8_t* tr = trash + lane * DPL;
     const bool lane_ok = rowok && (EXACT || p * DPL < g.D);
+    const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
     HChunk16 cur = hload16<DPL, DX>(cLr, cRr, g, 0, p);
     HChunk16 nxt = cur;
     for (int b = 0; b * U < n; b++) {
@@ -247,7 +252,9 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
             p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; },
                                  P1P1, P2P2, imask, Labs);
             const int x1 = DX > 0 ? i : n - 1 - i;
-            store_pairs<DPL>((lane_ok && i < n) ? rowbase + (size_t)x1 * g.D : tr, Labs);
+            const bool ok = lane_ok && i < n;
+            uint8_t* dst = ok ? rowbase + (size_t)x1 * g.D : tr;
+            store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
             if constexpr (DX > 0) {
                 constexpr int ph = ((DPL - 1 - t) % DPL + DPL) % DPL;
                 cr[ph] = row_shr1_u64(cr[ph], inj);
@@ -334,6 +341,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     for (int i = 0; i < M; i++) Lr[i] = start[i];
     bool pv = false;
     const bool lane_act = EXACT || p * DPL < g.D;
+    const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
     // stores: 32-bit offsets from the wave-uniform volume base (cells or the trash slot)
     const uint32_t tr_off = (uint32_t)(trash - V) + (uint32_t)((tid & 63) * DPL);
     const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
@@ -356,9 +364,10 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         // lowered to "0" (kBase), which clamps every candidate: one select per step.
         const uint32_t P2x = pv ? P2P2 : kBaseP2;
         p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
-        const uint32_t off = (valid && lane_act)
+        const bool ok = valid && lane_act;
+        const uint32_t off = ok
             ? (uint32_t)((min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL) : tr_off;
-        store_pairs<DPL>(V + off, Labs);
+        store_pairs<DPL>(V + off, V + ((ok && hi_ok) ? off + 16 : tr_off + 16), Labs);
         pv = valid;
     };
     for (int s = s0; s < s1; s += 2) {
@@ -389,13 +398,22 @@ __device__ __forceinline__ void paths_block16(const uint64_t* __restrict__ cL, c
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_paths16(const uint64_t* __restrict__ cL,
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4))) void k_census_paths16(const uint64_t* __restrict__ cL,
                                                         const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
                                                         size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                                                        const uint32_t* __restrict__ items)
+                                                        const uint32_t* __restrict__ items,
+                                                        uint64_t* __restrict__ trace)
 {
     __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
+    const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     paths_block16<DPL, EXACT>(cL, cR, vols, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
+    if (trace && (threadIdx.x & 63) == 0) {        // debug timeline (SGM_TRACE): one record per wave
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
+        uint64_t* r = trace + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+        r[0] = items[blockIdx.x] | ((uint64_t)blockIdx.x << 32); r[1] = ((uint64_t)xcc << 32) | hw; r[2] = t0; r[3] = t1;
+    }
 }
 
 // ====================================================================================
@@ -534,7 +552,7 @@ __global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict_
 // the path work list.
 // ------------------------------------------------------------------------------------
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_fused16(const uint64_t* __restrict__ cL,
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4))) void k_census_fused16(const uint64_t* __restrict__ cL,
                                                         const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols_p,
                                                         size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
                                                         const uint32_t* __restrict__ items, int n_items,
@@ -617,13 +635,32 @@ static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vo
                              size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
                              int n_items, hipStream_t st)
 {
+    // SGM_TRACE=<file>: debug timeline of the path launch (one record per wave), written
+    // after a synchronise. Never set in production runs.
+    static uint64_t* trace = nullptr;
+    static size_t trace_n = 0;
+    const char* tpath = getenv("SGM_TRACE");
+    if (tpath && trace_n < (size_t)n_items * 16) {
+        if (trace) (void)hipFree(trace);
+        trace_n = (size_t)n_items * 16;
+        if (hipMalloc(&trace, trace_n * 8) != hipSuccess) { trace = nullptr; trace_n = 0; }
+    }
+    uint64_t* tr = tpath ? trace : nullptr;
     dim3 grid(n_items), block(kWG);
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl,
-                           items);
+                           items, tr);
     else
         hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g,
-                           pl, items);
+                           pl, items, tr);
+    if (tr) {
+        std::vector<uint64_t> h((size_t)n_items * 16);
+        if (hipStreamSynchronize(st) == hipSuccess &&
+            hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            FILE* f = fopen(tpath, "wb");
+            if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
+        }
+    }
 }
 
 // Each volume slice is vol_bytes long: H*width1*D cells followed by a trash slot.

@@ -41,7 +41,7 @@ using sgm::Geom;
 namespace {
 
 constexpr size_t kAlign = 256;
-constexpr size_t kTrashBytes = 4096;   // >= 64 lanes x 8 disparities (census_sgm.hip)
+constexpr size_t kTrashBytes = 4096;   // >= 64 lanes x 32 disparities (census_sgm.hip trash stores)
 inline size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
 // effective parameters — identical rules to the oracle (oracle/sgm_oracle.c effective())

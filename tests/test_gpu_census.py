@@ -20,7 +20,8 @@ def test_census_codes(engine, oracle, shape):
     assert np.array_equal(engine.census(img), oracle.census(img))
 
 
-@pytest.mark.parametrize("D,minD", [(16, 0), (32, -7), (64, 3), (128, 0), (256, 0), (512, 0), (48, 2), (80, -3)])
+@pytest.mark.parametrize("D,minD", [(16, 0), (32, -7), (64, 3), (128, 0), (256, 0), (512, 0), (48, 2), (80, -3),
+                                    (272, 0), (400, -5)])
 @pytest.mark.parametrize("dirn", range(8))
 def test_census_path_volumes(engine, oracle, synth, pkg, dirn, D, minD):
     h = 23
@@ -45,6 +46,7 @@ CASES = [
     dict(num_disparities=256, uniqueness_ratio=0),
     dict(num_disparities=512),
     dict(num_disparities=64, p2=250),         # clamped to 193 (u8 path costs)
+    dict(num_disparities=400, min_disparity=3),   # D % 32 == 16: a lane straddles D (DPL 32)
 ]
 
 

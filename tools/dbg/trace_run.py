@@ -1,0 +1,15 @@
+"""Run the C3 path launch with SGM_TRACE set (debug timeline), several variants."""
+import os, sys, subprocess
+sys.path.insert(0, "."); sys.path.insert(0, "tests")
+import numpy as np
+import __graft_entry__ as ge
+from conftest import _load
+pkg = ge.load_package()
+synth = _load("sgm_synth", ge.PKG_DIR + "/synth.py")
+eng = pkg.Engine(0)
+left, right, _ = synth.stereo_pair(1080, 1920, 0, 256, seed=1)
+eng.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=256))
+out = os.environ["SGM_TRACE"]
+for rep in range(3):
+    eng.match(left, right)
+print("ok", os.path.getsize(out))
