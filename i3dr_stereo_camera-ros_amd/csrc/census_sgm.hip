@@ -181,8 +181,18 @@ __device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL /
 struct PathLaunch16 {
     int xb_lo[6];        // row sweeps: first base column of the direction
 };
-// Work list entry of k_census_paths16 (one per workgroup): dir << 24 | local block.
-__host__ __device__ constexpr uint32_t path_item(int dir, int lb) { return ((uint32_t)dir << 24) | (uint32_t)lb; }
+// Work list entry (one per workgroup): dir << 24 | frame-in-group << 22 | local block.
+__host__ __device__ constexpr uint32_t path_item(int dir, int lb, int f = 0)
+{
+    return ((uint32_t)dir << 24) | ((uint32_t)f << 22) | (uint32_t)lb;
+}
+
+// wave-uniform pick from a kernel-argument array without dynamic indexing (no scratch)
+template <typename T>
+__device__ __forceinline__ T pick4(const T (&a)[kMaxGroup], int f)
+{
+    return f == 0 ? a[0] : f == 1 ? a[1] : f == 2 ? a[2] : a[3];
+}
 
 constexpr int kWG = 256;          // 4 waves
 constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
@@ -382,15 +392,18 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     }
 }
 
-// One work-list entry: 16 lines of one direction (lds: 2 * RowSeg<DPL>::BUF u64).
+// One work-list entry: 16 lines of one direction of one frame (lds: 2 * RowSeg<DPL>::BUF).
 template <int DPL, bool EXACT>
-__device__ __forceinline__ void paths_block16(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
-                                              uint8_t* __restrict__ vols, size_t vol_bytes, size_t trash_off,
+__device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_bytes, size_t trash_off,
                                               const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
     const int dir = (int)(it >> 24);
-    const int lb = (int)(it & 0xFFFFFFu);
-    uint8_t* V = vols + (size_t)dir * vol_bytes;
+    const int f = (int)((it >> 22) & 3u);
+    const int lb = (int)(it & 0x3FFFFFu);
+    if (f >= pf.n) return;                          // uniform over the workgroup
+    const uint64_t* cL = pick4(pf.cL, f);
+    const uint64_t* cR = pick4(pf.cR, f);
+    uint8_t* V = pick4(pf.vols, f) + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
@@ -398,15 +411,13 @@ __device__ __forceinline__ void paths_block16(const uint64_t* __restrict__ cL, c
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4))) void k_census_paths16(const uint64_t* __restrict__ cL,
-                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols,
-                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                                                        const uint32_t* __restrict__ items,
-                                                        uint64_t* __restrict__ trace)
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
+void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
+                      const uint32_t* __restrict__ items, uint64_t* __restrict__ trace)
 {
     __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    paths_block16<DPL, EXACT>(cL, cR, vols, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
+    paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
     if (trace && (threadIdx.x & 63) == 0) {        // debug timeline (SGM_TRACE): one record per wave
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
@@ -538,34 +549,39 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
+// block b: row b % H of frame b / H
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_wta16(const uint8_t* __restrict__ vols, size_t vol_bytes, Geom g,
-                                                      int16_t* __restrict__ out, size_t out_stride)
+__device__ __forceinline__ void wta_block16(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride,
+                                            int b, uint32_t* lds)
+{
+    const int f = b / g.H;
+    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, b - f * g.H, lds);
+}
+
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_bytes, Geom g, size_t out_stride)
 {
     extern __shared__ uint32_t lds_dyn[];
-    wta_row16<DPL, EXACT>(vols, vol_bytes, g, out, out_stride, blockIdx.x, lds_dyn);
+    wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn);
 }
 
 // ------------------------------------------------------------------------------------
-// Frame pipelining: one launch runs the path sweeps of frame i+1 (VALU-bound) and the WTA
-// rows of frame i (HBM-bound). Blocks [wta_at, wta_at + H) are WTA rows, the others walk
-// the path work list.
+// Frame pipelining: one launch runs the path sweeps of a group of frames (VALU-bound) and
+// the WTA rows of the previous group (HBM-bound). Blocks [0, n_items) walk the path work
+// list (longest first, frames interleaved: more blocks than resident slots, so the
+// hardware dispatcher balances the CUs), the blocks after them are WTA rows, which fill
+// the CUs the path sweeps' tail leaves idle (measured at C3 for one frame: WTA first
+// 2.02 ms, interleaved 1.97, evenly from 30 % 1.92, last 1.71).
 // ------------------------------------------------------------------------------------
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4))) void k_census_fused16(const uint64_t* __restrict__ cL,
-                                                        const uint64_t* __restrict__ cR, uint8_t* __restrict__ vols_p,
-                                                        size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                                                        const uint32_t* __restrict__ items, int n_items,
-                                                        const uint8_t* __restrict__ vols_w, int16_t* __restrict__ out,
-                                                        size_t out_stride, int wta_at)
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
+void k_census_fused16(PathFrames pf, WtaFrames wf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
+                      const uint32_t* __restrict__ items, int n_items, size_t out_stride)
 {
     extern __shared__ uint64_t lds_dyn64[];
     const int b = blockIdx.x;
-    if (b >= wta_at && b < wta_at + g.H)
-        wta_row16<DPL, EXACT>(vols_w, vol_bytes, g, out, out_stride, b - wta_at, (uint32_t*)lds_dyn64);
-    else
-        paths_block16<DPL, EXACT>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items[b < wta_at ? b : b - g.H],
-                                  lds_dyn64);
+    if (b >= n_items) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, b - n_items, (uint32_t*)lds_dyn64);
+    else paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64);
 }
 
 // ------------------------------------------------------------------------------------
@@ -588,21 +604,24 @@ PathLaunch16 make_path_launch16(const Geom& g)
     return pl;
 }
 
-// Work list of one paths launch: every workgroup of every direction (only_dir >= 0: that
-// direction only), longest first, dealt out in a snake over rounds of n_slots workgroups.
-// The hardware hands consecutive workgroup ids to different CUs, so each CU ends up with a
-// mix of long (horizontal, vertical) and short (diagonal corner) work instead of several
-// long ones — the kernel's tail is the most loaded CU.
-int census_path_items(const Geom& g, int only_dir, int n_slots, uint32_t* out, int cap)
+// Work list of one paths launch for a group of `group` frames: every 16-line block of
+// every direction (only_dir >= 0: that direction only) of every frame, longest first with
+// the frames of equal-length blocks adjacent, dealt in a snake over rounds of n_slots
+// workgroups (consecutive workgroup ids go to different CUs, so each CU mixes long and
+// short work; with group > 1 there are more blocks than resident slots and the dispatcher
+// hands the short ones to whichever CUs drain first).
+int census_path_items(const Geom& g, int only_dir, int n_slots, int group, uint32_t* out, int cap)
 {
     struct Item { int len; uint32_t code; };
     std::vector<Item> v;
     const PathLaunch16 pl = make_path_launch16(g);
+    group = std::min(std::max(group, 1), kMaxGroup);
     for (int dir = 0; dir < 8; dir++) {
         if (only_dir >= 0 && dir != only_dir) continue;
         if (dir >= 6) {
             const int nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
-            for (int b = 0; b < nb; b++) v.push_back({g.width1, path_item(dir, b)});
+            for (int b = 0; b < nb; b++)
+                for (int f = 0; f < group; f++) v.push_back({g.width1, path_item(dir, b, f)});
             continue;
         }
         const int rx = dir_rx(dir);
@@ -614,7 +633,7 @@ int census_path_items(const Geom& g, int only_dir, int n_slots, uint32_t* out, i
             if (rx == 0) { s0 = 0; s1 = g.H; }
             else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
             else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + kColsPerWG - g.minX1); }
-            v.push_back({std::max(s1 - s0, 0), path_item(dir, b)});
+            for (int f = 0; f < group; f++) v.push_back({std::max(s1 - s0, 0), path_item(dir, b, f)});
         }
     }
     const int n = (int)v.size();
@@ -631,9 +650,8 @@ int census_path_items(const Geom& g, int only_dir, int n_slots, uint32_t* out, i
 }
 
 template <int DPL>
-static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
-                             size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
-                             int n_items, hipStream_t st)
+static void launch_paths_dpl(const PathFrames& pf, size_t vol_bytes, size_t trash_off, const Geom& g,
+                             const PathLaunch16& pl, const uint32_t* items, int n_items, hipStream_t st)
 {
     // SGM_TRACE=<file>: debug timeline of the path launch (one record per wave), written
     // after a synchronise. Never set in production runs.
@@ -648,11 +666,11 @@ static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vo
     uint64_t* tr = tpath ? trace : nullptr;
     dim3 grid(n_items), block(kWG);
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g, pl,
-                           items, tr);
+        hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, pf, vol_bytes, trash_off, g, pl, items,
+                           tr);
     else
-        hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, cL, cR, vols, vol_bytes, trash_off, g,
-                           pl, items, tr);
+        hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, pf, vol_bytes, trash_off, g, pl, items,
+                           tr);
     if (tr) {
         std::vector<uint64_t> h((size_t)n_items * 16);
         if (hipStreamSynchronize(st) == hipSuccess &&
@@ -663,81 +681,76 @@ static void launch_paths_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vo
     }
 }
 
-// Each volume slice is vol_bytes long: H*width1*D cells followed by a trash slot.
-// items: device copy of census_path_items() for this geometry (n_items entries).
-hipError_t launch_census_paths(const uint64_t* cL, const uint64_t* cR, uint8_t* vols, size_t vol_bytes,
-                               const Geom& g, const uint32_t* items, int n_items, hipStream_t st)
+// Path sweeps of the frames in pf (codes -> volumes). Each volume slice is vol_bytes long:
+// H*width1*D cells followed by a trash slot. items: device copy of census_path_items().
+hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geom& g, const uint32_t* items,
+                               int n_items, hipStream_t st)
 {
     if (n_items <= 0) return hipSuccess;
     const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
-    case 2: launch_paths_dpl<2>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
-    case 4: launch_paths_dpl<4>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
-    case 8: launch_paths_dpl<8>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
-    case 16: launch_paths_dpl<16>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
-    default: launch_paths_dpl<32>(cL, cR, vols, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 2: launch_paths_dpl<2>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 4: launch_paths_dpl<4>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 8: launch_paths_dpl<8>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    case 16: launch_paths_dpl<16>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;
+    default: launch_paths_dpl<32>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;
     }
     return hipGetLastError();
 }
 
 template <int DPL>
-static void launch_wta_dpl(const uint8_t* vols, size_t vol_bytes, const Geom& g, int16_t* out, size_t out_stride,
-                           hipStream_t st)
+static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
 {
-    dim3 grid(g.H), block(kWG);
+    dim3 grid(g.H * wf.n), block(kWG);
     const size_t lds = wta_lds_bytes<DPL>(g.W);
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, vols, vol_bytes, g, out, out_stride);
+        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
     else
-        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, vols, vol_bytes, g, out, out_stride);
+        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
 }
 
-hipError_t launch_census_wta(const uint8_t* vols, size_t vol_bytes, const Geom& g, int16_t* out, size_t out_stride,
-                             hipStream_t st)
+// WTA + LR of the frames in wf (volumes -> disparity).
+hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
 {
     switch (dpl16_for(g.D)) {
-    case 2: launch_wta_dpl<2>(vols, vol_bytes, g, out, out_stride, st); break;
-    case 4: launch_wta_dpl<4>(vols, vol_bytes, g, out, out_stride, st); break;
-    case 8: launch_wta_dpl<8>(vols, vol_bytes, g, out, out_stride, st); break;
-    case 16: launch_wta_dpl<16>(vols, vol_bytes, g, out, out_stride, st); break;
-    default: launch_wta_dpl<32>(vols, vol_bytes, g, out, out_stride, st); break;
+    case 2: launch_wta_dpl<2>(wf, vol_bytes, g, out_stride, st); break;
+    case 4: launch_wta_dpl<4>(wf, vol_bytes, g, out_stride, st); break;
+    case 8: launch_wta_dpl<8>(wf, vol_bytes, g, out_stride, st); break;
+    case 16: launch_wta_dpl<16>(wf, vol_bytes, g, out_stride, st); break;
+    default: launch_wta_dpl<32>(wf, vol_bytes, g, out_stride, st); break;
     }
     return hipGetLastError();
 }
 
 template <int DPL>
-static void launch_fused_dpl(const uint64_t* cL, const uint64_t* cR, uint8_t* vols_p, size_t vol_bytes,
-                             size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
-                             int n_items, const uint8_t* vols_w, int16_t* out, size_t out_stride, hipStream_t st)
+static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, size_t trash_off,
+                             const Geom& g, const PathLaunch16& pl, const uint32_t* items, int n_items,
+                             size_t out_stride, hipStream_t st)
 {
-    dim3 grid(n_items + g.H), block(kWG);
+    dim3 grid(n_items + g.H * wf.n), block(kWG);
     const size_t lds = std::max(wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF);
-    // WTA rows after all path blocks: they fill the CUs the path sweeps' tail leaves idle
-    // (measured at C3: WTA first 2.02 ms, interleaved 1.97, evenly from 30 % 1.92, last 1.71)
-    const int wta_at = n_items;
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, cL, cR, vols_p, vol_bytes, trash_off,
-                           g, pl, items, n_items, vols_w, out, out_stride, wta_at);
+        hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
+                           items, n_items, out_stride);
     else
-        hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, cL, cR, vols_p, vol_bytes, trash_off,
-                           g, pl, items, n_items, vols_w, out, out_stride, wta_at);
+        hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
+                           items, n_items, out_stride);
 }
 
-// Paths of one frame (codes cL/cR -> volumes vols_p) fused with the WTA of the previous
-// frame (volumes vols_w -> out). Both volume sets have the same geometry.
-hipError_t launch_census_fused(const uint64_t* cL, const uint64_t* cR, uint8_t* vols_p, size_t vol_bytes,
-                               const Geom& g, const uint32_t* items, int n_items, const uint8_t* vols_w,
-                               int16_t* out, size_t out_stride, hipStream_t st)
+// Path sweeps of the frames in pf fused with the WTA of the frames in wf (the previous
+// group). All volume sets have the same geometry.
+hipError_t launch_census_fused(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, const Geom& g,
+                               const uint32_t* items, int n_items, size_t out_stride, hipStream_t st)
 {
     const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
-    case 2: launch_fused_dpl<2>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
-    case 4: launch_fused_dpl<4>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
-    case 8: launch_fused_dpl<8>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
-    case 16: launch_fused_dpl<16>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
-    default: launch_fused_dpl<32>(cL, cR, vols_p, vol_bytes, trash_off, g, pl, items, n_items, vols_w, out, out_stride, st); break;
+    case 2: launch_fused_dpl<2>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 4: launch_fused_dpl<4>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 8: launch_fused_dpl<8>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 16: launch_fused_dpl<16>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    default: launch_fused_dpl<32>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
     }
     return hipGetLastError();
 }

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -21,12 +22,11 @@
 
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
-int census_path_items(const Geom&, int, int, uint32_t*, int);
-hipError_t launch_census_paths(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, const uint32_t*, int,
+int census_path_items(const Geom&, int, int, int, uint32_t*, int);
+hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t);
+hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
+hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, size_t, const Geom&, const uint32_t*, int, size_t,
                                hipStream_t);
-hipError_t launch_census_wta(const uint8_t*, size_t, const Geom&, int16_t*, size_t, hipStream_t);
-hipError_t launch_census_fused(const uint64_t*, const uint64_t*, uint8_t*, size_t, const Geom&, const uint32_t*, int,
-                               const uint8_t*, int16_t*, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -116,7 +116,7 @@ struct sgm_handle {
     int n_cu = 0;                  // compute units of the device (path work-list dealing)
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
-    std::string items_key;         // geometry + workspace the device copy belongs to
+    std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
 };
 
 namespace {
@@ -171,7 +171,8 @@ int stage_index(sgm_handle* h, const char* name, double bytes)
 int ensure_ws(sgm_handle* h, size_t bytes)
 {
     if (h->ws.size >= bytes) return SGM_OK;
-    h->items_key.clear();          // contents (the path work list) do not survive
+    h->items_key[0].clear();       // contents (the path work lists) do not survive
+    h->items_key[1].clear();
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
         (void)hipFree(h->ws.base);
@@ -199,16 +200,18 @@ int ensure_pin(sgm_handle* h, size_t bytes)
 
 // Workspace carve-up for one geometry. Offsets are 256-B aligned.
 struct Layout {
-    size_t cL = 0, cR = 0, vols = 0, vol_bytes = 0;       // census
-    size_t items = 0; int n_items = 0;                     // census path work list
-    size_t cL2 = 0, cR2 = 0, vols2 = 0;                    // census: second set (pipelined batch)
+    // census: set 0 serves single matches; a pipelined batch uses sets 0 .. 2*group-1
+    size_t cL[2 * sgm::kMaxGroup] = {}, cR[2 * sgm::kMaxGroup] = {}, vols[2 * sgm::kMaxGroup] = {};
+    size_t vol_bytes = 0;
+    int group = 1;                                         // frames per pipelined launch
+    size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovol_elems = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0;                      // host-API staging
     size_t total = 0;
 };
 
-Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, bool two_sets = false)
+Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group = 0)
 {
     Layout l;
     size_t off = 0;
@@ -216,18 +219,21 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, bool two_se
     const size_t WH = (size_t)g.W * g.H;
     const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
     if (p.mode == SGM_MODE_CENSUS8) {
-        l.cL = take(WH * 8);
-        l.cR = take(WH * 8);
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
-        l.vols = take(l.vol_bytes * 8);
-        if (g.width1 > 0) {
-            l.n_items = sgm::census_path_items(g, -1, 1, nullptr, 0);
-            l.items = take((size_t)l.n_items * 4);
+        l.group = std::max(group, 1);
+        const int sets = group > 0 ? 2 * l.group : 1;
+        for (int i = 0; i < sets; i++) {
+            l.cL[i] = take(WH * 8);
+            l.cR[i] = take(WH * 8);
+            l.vols[i] = take(l.vol_bytes * 8);
         }
-        if (two_sets) {
-            l.cL2 = take(WH * 8);
-            l.cR2 = take(WH * 8);
-            l.vols2 = take(l.vol_bytes * 8);
+        if (g.width1 > 0) {
+            l.n_items[0] = sgm::census_path_items(g, -1, 1, 1, nullptr, 0);
+            l.items[0] = take((size_t)l.n_items[0] * 4);
+            if (group > 0) {
+                l.n_items[1] = sgm::census_path_items(g, -1, 1, l.group, nullptr, 0);
+                l.items[1] = take((size_t)l.n_items[1] * 4);
+            }
         }
     } else {
         l.planes = take(WH * 4);
@@ -236,7 +242,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, bool two_se
         l.ovol_elems = align_up(cells * 2) / 2;
         l.ovols = take(l.ovol_elems * 2 * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5));
     }
-    l.tmp = take(WH * 2);
+    l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
     if (host_io) { l.inL = take(WH); l.inR = take(WH); l.out = take(WH * 2); }
     l.total = off;
@@ -270,15 +276,17 @@ struct StageRec {
 
 // Device work list of the census path launch for (g, only_dir), uploaded on `st` when the
 // geometry or the workspace changed. Returns the entry count (< 0: error).
-int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, hipStream_t st, const uint32_t** dev)
+int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, int group, hipStream_t st,
+               const uint32_t** dev)
 {
-    uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items);
+    const int w = group > 1 ? 1 : 0;
+    uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items[w]);
     *dev = d;
     char key[160];
-    snprintf(key, sizeof key, "%d %d %d %d %d %d %p", g.W, g.H, g.D, g.minD, only_dir, h->n_cu, (void*)d);
-    const int n = sgm::census_path_items(g, only_dir, h->n_cu, nullptr, 0);
-    if (h->items_key == key) return n;
-    if (n > l.n_items) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
+    snprintf(key, sizeof key, "%d %d %d %d %d %d %d %p", g.W, g.H, g.D, g.minD, only_dir, group, h->n_cu, (void*)d);
+    const int n = sgm::census_path_items(g, only_dir, h->n_cu, group, nullptr, 0);
+    if (h->items_key[w] == key) return n;
+    if (n > l.n_items[w]) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
     if (n > h->items_cap) {
         if (h->items_pin) (void)hipHostFree(h->items_pin);
         h->items_pin = nullptr;
@@ -286,22 +294,26 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, hipS
         HIP_TRY(hipHostMalloc((void**)&h->items_pin, (size_t)n * 4, hipHostMallocDefault), "hipHostMalloc");
         h->items_cap = n;
     }
-    sgm::census_path_items(g, only_dir, h->n_cu, h->items_pin, h->items_cap);
+    sgm::census_path_items(g, only_dir, h->n_cu, group, h->items_pin, h->items_cap);
     HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
     HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
-    h->items_key = key;
+    h->items_key[w] = key;
     return n;
 }
 
 // Post filters of one finished frame (src = the WTA output in `tmp` when a median runs).
-int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_t out_stride, StageRec& rec)
+// tmp_off: element offset of this frame's raw image in `tmp` (a pipelined group holds one
+// raw image per frame).
+int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_t out_stride, StageRec& rec,
+             size_t tmp_off = 0)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
     const double WH = (double)g.W * g.H;
     if (use_median(p)) {
         rec.begin("median3", 4 * WH);
-        HIP_TRY(sgm::launch_median3((int16_t*)(ws + l.tmp), g.W, dOut, out_stride, g.W, g.H, h->stream), "median3");
+        HIP_TRY(sgm::launch_median3((int16_t*)(ws + l.tmp) + tmp_off, g.W, dOut, out_stride, g.W, g.H, h->stream),
+                "median3");
     }
     if (p.speckle_window_size > 0) {
         rec.begin("speckle", 14 * WH);
@@ -332,18 +344,22 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("fill_invalid", 2 * WH);
         HIP_TRY(sgm::launch_fill16(dst, dst_stride, g.W, g.H, g.invalid, st), "fill");
     } else if (p.mode == SGM_MODE_CENSUS8) {
-        uint64_t* cL = (uint64_t*)(ws + l.cL);
-        uint64_t* cR = (uint64_t*)(ws + l.cR);
-        uint8_t* vols = (uint8_t*)(ws + l.vols);
+        uint64_t* cL = (uint64_t*)(ws + l.cL[0]);
+        uint64_t* cR = (uint64_t*)(ws + l.cR[0]);
+        uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
         rec.begin("census", 2 * WH + 16 * WH);
         HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
         const uint32_t* items;
-        const int n_items = path_items(h, l, g, -1, st, &items);
+        const int n_items = path_items(h, l, g, -1, 1, st, &items);
         if (n_items < 0) return n_items;
+        sgm::PathFrames pf{};
+        pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
+        sgm::WtaFrames wf{};
+        wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
         rec.begin("paths8", 8 * cells);
-        HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, items, n_items, st), "paths");
+        HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
-        HIP_TRY(sgm::launch_census_wta(vols, l.vol_bytes, g, dst, dst_stride, st), "wta");
+        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -364,8 +380,19 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
     return SGM_OK;
 }
 
-// Census-mode frame pipeline over n >= 2 frames on h->stream (two workspace sets):
-//   census(0) paths(0) | census(i) fused[paths(i) + wta(i-1)] post(i-1) ... | wta(n-1) post(n-1)
+// Frames per pipelined launch: 2 (more path blocks than resident workgroup slots, so the
+// dispatcher balances the CUs) unless the batch is shorter; SGM_GROUP overrides (1..4).
+int batch_group(int n)
+{
+    const char* env = std::getenv("SGM_GROUP");
+    const int g = env ? std::atoi(env) : 2;
+    return std::max(1, std::min({g, sgm::kMaxGroup, n}));
+}
+
+// Census-mode frame pipeline on h->stream, in groups of l.group frames (sets 2*group):
+//   census(G0) paths(G0) | census(Gk) fused[paths(Gk) + wta(Gk-1)] post(Gk-1) ... | wta(Glast) post
+// With a median the WTA of a group writes each frame's raw disparity to its own scratch
+// image (post filters read it), so no frame's output is overwritten before its median.
 int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* const* dLs,
                      const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride)
 {
@@ -375,55 +402,76 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
     const bool med = use_median(p);
     const double WH = (double)g.W * g.H;
     const double cells = (double)g.width1 * g.H * g.D;
-    uint64_t* cL[2] = {(uint64_t*)(ws + l.cL), (uint64_t*)(ws + l.cL2)};
-    uint64_t* cR[2] = {(uint64_t*)(ws + l.cR), (uint64_t*)(ws + l.cR2)};
-    uint8_t* vols[2] = {(uint8_t*)(ws + l.vols), (uint8_t*)(ws + l.vols2)};
-    int16_t* tmp = (int16_t*)(ws + l.tmp);
+    const int G = l.group;
+    const int ng = (n + G - 1) / G;
     const uint32_t* items;
-    const int n_items = path_items(h, l, g, -1, st, &items);
+    const int n_items = path_items(h, l, g, -1, G, st, &items);
     if (n_items < 0) return n_items;
     StageRec rec{h};
     if (h->profiling) h->prof_frames += n;
-    for (int i = 0; i <= n; i++) {
-        const int s = i & 1;
-        if (i < n) {
-            rec.begin("census", 2 * WH + 16 * WH);
-            HIP_TRY(sgm::launch_census(dLs[i], dRs[i], stride, g.W, g.H, cL[s], cR[s], st), "census");
+    auto frames_of = [&](int k) { return std::min(G, n - k * G); };
+    auto path_frames = [&](int k) {
+        sgm::PathFrames pf{};
+        pf.n = frames_of(k);
+        for (int f = 0; f < pf.n; f++) {
+            const int set = (k & 1) * G + f;
+            pf.cL[f] = (const uint64_t*)(ws + l.cL[set]);
+            pf.cR[f] = (const uint64_t*)(ws + l.cR[set]);
+            pf.vols[f] = (uint8_t*)(ws + l.vols[set]);
         }
-        int16_t* dst = nullptr;
-        size_t dst_stride = 0;
-        if (i > 0) {
-            dst = med ? tmp : outs[i - 1];
-            dst_stride = med ? (size_t)g.W : out_stride;
+        return pf;
+    };
+    size_t dst_stride = med ? (size_t)g.W : out_stride;
+    auto wta_frames = [&](int k) {
+        sgm::WtaFrames wf{};
+        wf.n = frames_of(k);
+        for (int f = 0; f < wf.n; f++) {
+            wf.vols[f] = (const uint8_t*)(ws + l.vols[(k & 1) * G + f]);
+            wf.out[f] = med ? (int16_t*)(ws + l.tmp) + (size_t)f * g.W * g.H : outs[k * G + f];
         }
-        if (i == 0) {
-            rec.begin("paths8", 8 * cells);
-            HIP_TRY(sgm::launch_census_paths(cL[s], cR[s], vols[s], l.vol_bytes, g, items, n_items, st), "paths");
-        } else if (i < n) {
-            rec.begin("paths8+wta_lr", 16 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_fused(cL[s], cR[s], vols[s], l.vol_bytes, g, items, n_items, vols[s ^ 1], dst,
+        return wf;
+    };
+    for (int k = 0; k <= ng; k++) {
+        if (k < ng) {
+            for (int f = 0; f < frames_of(k); f++) {
+                const int set = (k & 1) * G + f;
+                rec.begin("census", 2 * WH + 16 * WH);
+                HIP_TRY(sgm::launch_census(dLs[k * G + f], dRs[k * G + f], stride, g.W, g.H,
+                                           (uint64_t*)(ws + l.cL[set]), (uint64_t*)(ws + l.cR[set]), st),
+                        "census");
+            }
+        }
+        if (k == 0) {
+            rec.begin("paths8", 8 * cells * frames_of(0));
+            HIP_TRY(sgm::launch_census_paths(path_frames(0), l.vol_bytes, g, items, n_items, st), "paths");
+        } else if (k < ng) {
+            rec.begin("paths8+wta_lr", (16 * cells + 2 * WH) * G);
+            HIP_TRY(sgm::launch_census_fused(path_frames(k), wta_frames(k - 1), l.vol_bytes, g, items, n_items,
                                              dst_stride, st), "fused");
         } else {
-            rec.begin("wta_lr", 8 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_wta(vols[s ^ 1], l.vol_bytes, g, dst, dst_stride, st), "wta");
+            rec.begin("wta_lr", (8 * cells + 2 * WH) * frames_of(k - 1));
+            HIP_TRY(sgm::launch_census_wta(wta_frames(k - 1), l.vol_bytes, g, dst_stride, st), "wta");
         }
-        if (i > 0) {
-            int rc = run_post(h, l, g, outs[i - 1], out_stride, rec);
-            if (rc) return rc;
+        if (k > 0) {
+            const int k1 = k - 1;
+            for (int f = 0; f < frames_of(k1); f++) {
+                int rc = run_post(h, l, g, outs[k1 * G + f], out_stride, rec, (size_t)f * g.W * g.H);
+                if (rc) return rc;
+            }
         }
     }
     rec.end();
     return SGM_OK;
 }
 
-int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, bool two_sets = false)
+int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int group = 0)
 {
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
     if ((rc = ensure_stream(h))) return rc;
-    l = make_layout(h->params, g, host_io, two_sets);
+    l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
-    if (h->params.mode != SGM_MODE_CENSUS8) h->items_key.clear();
+    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
     return ensure_ws(h, l.total);
 }
 
@@ -538,14 +586,14 @@ int sgm_match_device_batch(sgm_handle* h, const uint8_t* const* dLs, const uint8
     if (n == 0) return SGM_OK;
     Geom g;
     Layout l;
-    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2;
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
-    rc = prepare(h, W, H, false, g, l, pipelined && g.width1 > 0);
+    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2 && g.width1 > 0;
+    rc = prepare(h, W, H, false, g, l, pipelined ? batch_group(n) : 0);
     if (rc) return rc;
     hipStream_t own = h->stream;
     if (stream) h->stream = (hipStream_t)stream;
-    if (pipelined && g.width1 > 0) {
+    if (pipelined) {
         rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride);
     } else {
         for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
@@ -722,15 +770,17 @@ int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int
     char* ws = (char*)h->ws.base;
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
     HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
-    uint64_t* cL = (uint64_t*)(ws + l.cL);
-    uint64_t* cR = (uint64_t*)(ws + l.cR);
-    uint8_t* vols = (uint8_t*)(ws + l.vols);
+    uint64_t* cL = (uint64_t*)(ws + l.cL[0]);
+    uint64_t* cR = (uint64_t*)(ws + l.cR[0]);
+    uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
     HIP_TRY(sgm::launch_census((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, W, H, cL, cR, h->stream),
             "census");
     const uint32_t* items;
-    const int n_items = path_items(h, l, g, dir, h->stream, &items);
+    const int n_items = path_items(h, l, g, dir, 1, h->stream, &items);
     if (n_items < 0) return n_items;
-    HIP_TRY(sgm::launch_census_paths(cL, cR, vols, l.vol_bytes, g, items, n_items, h->stream), "paths");
+    sgm::PathFrames pf{};
+    pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
+    HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, h->stream), "paths");
     const size_t cells = (size_t)g.width1 * g.H * g.D;
     HIP_TRY(hipMemcpyAsync(vol, vols + (size_t)dir * l.vol_bytes, cells, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");

@@ -219,6 +219,21 @@ __device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, con
 
 // LDS carve-up of the per-row WTA state: key u32 [W] | drow i16 | bst i16 | mins u16, the
 // last three with 64 extra dummy slots (index W + lane) for branch-free stores.
+// A group of frames handled by one launch (frame pipelining): per frame its census codes
+// and volume set (paths) or volume set and output (WTA). Frames >= n are skipped.
+constexpr int kMaxGroup = 4;
+struct PathFrames {
+    const uint64_t* cL[kMaxGroup];
+    const uint64_t* cR[kMaxGroup];
+    uint8_t* vols[kMaxGroup];
+    int n;
+};
+struct WtaFrames {
+    const uint8_t* vols[kMaxGroup];
+    int16_t* out[kMaxGroup];
+    int n;
+};
+
 struct RowLds {
     uint32_t* key; int16_t* drow; int16_t* bst; uint16_t* mins;
     static size_t bytes(int W) { return (size_t)4 * W + (size_t)6 * (W + 64) + 16; }
