@@ -68,11 +68,13 @@ class SgmParams(ctypes.Structure):
 _lib = None
 
 
-def load_library(path=LIB_PATH):
-    """Load libsgm_hip.so; raises if it is missing (no silent fallback)."""
+def load_library(path=None):
+    """Load libsgm_hip.so (SGM_HIP_LIB overrides the in-tree path, e.g. for an experimental
+    build); raises if it is missing (no silent fallback)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("SGM_HIP_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(f"libsgm_hip.so not found at {path}: run build() / build_ext.py first")
     # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7).

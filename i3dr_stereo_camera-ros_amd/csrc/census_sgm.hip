@@ -356,12 +356,17 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     const uint32_t tr_off = (uint32_t)(trash - V) + (uint32_t)((tid & 63) * DPL);
     const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
 
+    // Segments are staged in LDS (double buffer, one barrier per step) from registers loaded
+    // 3 steps ahead: the counted vmcnt wait for a segment then leaves the stores of the last
+    // three steps in flight (gfx950 retires loads and stores on one in-order counter).
     uint64_t* buf0 = lds;
     uint64_t* buf1 = lds + RS::BUF;
-    uint64_t A[RS::NLOAD], B[RS::NLOAD];
-    seg_load<DPL>(A, cL, cR, g, rx, ry, xb, s0, tid);
-    seg_store<DPL>((s0 & 1) ? buf1 : buf0, A, tid);
-    seg_load<DPL>(A, cL, cR, g, rx, ry, xb, min(s0 + 1, s1 - 1), tid);
+    uint64_t R0[RS::NLOAD], R1[RS::NLOAD], R2[RS::NLOAD], R3[RS::NLOAD];
+    seg_load<DPL>(R0, cL, cR, g, rx, ry, xb, s0, tid);
+    seg_store<DPL>(buf0, R0, tid);
+    seg_load<DPL>(R1, cL, cR, g, rx, ry, xb, min(s0 + 1, s1 - 1), tid);
+    seg_load<DPL>(R2, cL, cR, g, rx, ry, xb, min(s0 + 2, s1 - 1), tid);
+    seg_load<DPL>(R3, cL, cR, g, rx, ry, xb, min(s0 + 3, s1 - 1), tid);
     __syncthreads();
 
     auto step = [&](int s, const uint64_t* bufc) {
@@ -380,15 +385,20 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         store_pairs<DPL>(V + off, V + ((ok && hi_ok) ? off + 16 : tr_off + 16), Labs);
         pv = valid;
     };
-    for (int s = s0; s < s1; s += 2) {
-        seg_load<DPL>(B, cL, cR, g, rx, ry, xb, min(s + 2, s1 - 1), tid);
-        step(s, (s & 1) ? buf1 : buf0);
-        seg_store<DPL>(((s + 1) & 1) ? buf1 : buf0, A, tid);
+    // step s reads buf[s & 1] (holding segment s), then segment s + 1 (register set
+    // (s + 1) % 4) goes to buf[(s + 1) & 1] and set s % 4 is reloaded with segment s + 4
+    auto body = [&](int s, const uint64_t* bcur, uint64_t* bnext, uint64_t (&Rnext)[RS::NLOAD],
+                    uint64_t (&Rfree)[RS::NLOAD]) {
+        seg_load<DPL>(Rfree, cL, cR, g, rx, ry, xb, min(s + 4, s1 - 1), tid);
+        step(s, bcur);
+        seg_store<DPL>(bnext, Rnext, tid);
         __syncthreads();
-        seg_load<DPL>(A, cL, cR, g, rx, ry, xb, min(s + 3, s1 - 1), tid);
-        step(s + 1, ((s + 1) & 1) ? buf1 : buf0);
-        seg_store<DPL>((s & 1) ? buf1 : buf0, B, tid);
-        __syncthreads();
+    };
+    for (int s = s0; s < s1; s += 4) {
+        body(s, buf0, buf1, R1, R0);
+        body(s + 1, buf1, buf0, R2, R1);
+        body(s + 2, buf0, buf1, R3, R2);
+        body(s + 3, buf1, buf0, R0, R3);
     }
 }
 
