@@ -41,7 +41,7 @@ EXPORTS = [
     "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch",
     "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
-    "sgm_stage_launches", "sgm_debug_census",
+    "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_debug_census",
     "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
 ]
 
@@ -110,6 +110,11 @@ def load_library(path=None):
     L.sgm_stage_name.restype = ctypes.c_char_p
     L.sgm_stage_bytes.argtypes = [vp, ci]
     L.sgm_stage_launches.argtypes = [vp, ci]
+    L.sgm_disparity_to_msg.argtypes = [vp, vp, sz, ci, ci, ctypes.c_float, ctypes.c_float, vp, sz, vp]
+    L.sgm_calc_q.argtypes = [P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double)]
+    L.sgm_calc_q.restype = None
+    L.sgm_depth_points.argtypes = [vp, vp, sz, ci, ci, vp, sz, ci, P(ctypes.c_double), ctypes.c_double,
+                                   ctypes.c_double, vp, sz, vp, ci, vp, vp]
     L.sgm_stage_bytes.restype = ctypes.c_double
     L.sgm_debug_census.argtypes = [vp, vp, ci, ci, sz, vp]
     L.sgm_debug_census_path.argtypes = [vp, vp, vp, ci, ci, sz, ci, vp]
@@ -260,6 +265,25 @@ class Engine:
                  float(self.lib.sgm_stage_bytes(self.h, i))) for i in range(n)]
 
     # -- stage entry points (parity tests) -------------------------------------------------
+    # -- after the matcher (device pointers, async on `stream`) ------------------------------
+    def disparity_to_msg(self, d_disp, disp_stride, width, height, min_disparity, max_disparity, d_out, out_stride,
+                         stream=None):
+        """DisparityImage float image from the int16 x16 disparity (generate_disparity.cpp:426-452)."""
+        self._check(self.lib.sgm_disparity_to_msg(self.h, ctypes.c_void_p(d_disp), disp_stride, width, height,
+                                                  float(min_disparity), float(max_disparity), ctypes.c_void_p(d_out),
+                                                  out_stride, ctypes.c_void_p(stream) if stream else None))
+
+    def depth_points(self, d_disp, disp_stride, width, height, q5, depth_min, depth_max, d_color=None,
+                     color_stride=0, channels=0, d_depth=None, depth_stride=0, d_points=None, max_points=0,
+                     d_num_points=None, stream=None):
+        """disparity_to_depth.cpp:127-205; q5 = (Q23, Q03, Q13, Q32, Q33)."""
+        q = (ctypes.c_double * 5)(*[float(v) for v in q5])
+        vp = ctypes.c_void_p
+        self._check(self.lib.sgm_depth_points(self.h, vp(d_disp), disp_stride, width, height, vp(d_color),
+                                              color_stride, channels, q, float(depth_min), float(depth_max),
+                                              vp(d_depth), depth_stride, vp(d_points), max_points,
+                                              vp(d_num_points), vp(stream) if stream else None))
+
     def census(self, img):
         img = np.ascontiguousarray(img, np.uint8)
         h, w = img.shape
@@ -297,6 +321,49 @@ class Engine:
         h, w = d.shape
         self._check(self.lib.sgm_debug_speckle(self.h, _ptr(d), w, h, new_val, max_size, max_diff))
         return d
+
+
+def calc_q(K, P_right, P_left):
+    """calc_q (disparity_to_depth.cpp:62-84) through the C-ABI: 4x4 float64 Q."""
+    lib = load_library()
+    dv = ctypes.c_double
+    k = (dv * 9)(*np.asarray(K, np.float64).ravel())
+    pr = (dv * 12)(*np.asarray(P_right, np.float64).ravel())
+    pl = (dv * 12)(*np.asarray(P_left, np.float64).ravel())
+    q = (dv * 16)()
+    lib.sgm_calc_q(k, pr, pl, q)
+    return np.array(q[:], np.float64).reshape(4, 4)
+
+
+def q_terms(Q):
+    """The five Q entries the depth node uses (disparity_to_depth.cpp:134-138)."""
+    Q = np.asarray(Q, np.float64)
+    return (Q[2, 3], Q[0, 3], Q[1, 3], Q[3, 2], Q[3, 3])
+
+
+def disp_info_to_depth(engine, disp_image, color, Q, depth_min=0.0, depth_max=100.0, gen_point_cloud=True):
+    """dispInfoMsg2depthMsg (disparity_to_depth.cpp:94-218) on the GPU: the DisparityImage
+    float image (+ MONO8/BGR8 color) -> (depth float32 HxW, points Nx3 float32, rgba N)."""
+    import torch
+    d = torch.as_tensor(np.ascontiguousarray(disp_image, np.float32)).cuda()
+    h, w = d.shape
+    c = None
+    ch = 0
+    if color is not None:
+        c = torch.as_tensor(np.ascontiguousarray(color, np.uint8)).cuda()
+        ch = 1 if c.dim() == 2 else 3
+    depth = torch.empty((h, w), dtype=torch.float32, device="cuda")
+    pts = torch.empty((h * w if gen_point_cloud else 1, 4), dtype=torch.float32, device="cuda")
+    n = torch.zeros(1, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    engine.depth_points(d.data_ptr(), w, w, h, q_terms(Q), depth_min, depth_max,
+                        c.data_ptr() if c is not None else None, w * ch, ch, depth.data_ptr(), w,
+                        pts.data_ptr() if gen_point_cloud else None, h * w if gen_point_cloud else 0,
+                        n.data_ptr(), stream)
+    torch.cuda.current_stream().synchronize()
+    k = int(n.item())
+    p = pts[:k].cpu().numpy() if gen_point_cloud else np.zeros((0, 4), np.float32)
+    return depth.cpu().numpy(), p[:, :3].copy(), p[:, 3].copy().view(np.uint32)
 
 
 def right_matcher_params(p):

@@ -30,6 +30,9 @@ hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, size_t, cons
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
+hipError_t launch_disp_to_msg(const int16_t*, size_t, int, int, float, float, float*, size_t, hipStream_t);
+hipError_t launch_depth_points(const float*, size_t, int, int, const float*, double, double, const uint8_t*, size_t,
+                               int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
 hipError_t launch_ocv_paths(const int16_t*, int16_t*, size_t, const Geom&, int, hipStream_t);
@@ -114,6 +117,8 @@ struct sgm_handle {
     double stage_bytes[SGM_MAX_STAGES] = {};
     std::vector<sgm_handle*> sub;  // per-device handles for sgm_match_batch
     int n_cu = 0;                  // compute units of the device (path work-list dealing)
+    int* aux = nullptr;            // per-row counts / offsets of sgm_depth_points
+    size_t aux_n = 0;
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
     std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
@@ -526,6 +531,7 @@ void sgm_destroy(sgm_handle* h)
         if (h->ws.base) (void)hipFree(h->ws.base);
         if (h->pin) (void)hipHostFree(h->pin);
         if (h->items_pin) (void)hipHostFree(h->items_pin);
+        if (h->aux) (void)hipFree(h->aux);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
@@ -600,6 +606,68 @@ int sgm_match_device_batch(sgm_handle* h, const uint8_t* const* dLs, const uint8
     }
     h->stream = own;
     return rc;
+}
+
+int sgm_disparity_to_msg(sgm_handle* h, const int16_t* d_disp, size_t disp_stride, int W, int H, float min_disparity,
+                         float max_disparity, float* d_out, size_t out_stride, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!d_disp || !d_out || W <= 0 || H <= 0 || disp_stride < (size_t)W || out_stride < (size_t)W)
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    HIP_TRY(sgm::launch_disp_to_msg(d_disp, disp_stride, W, H, min_disparity, max_disparity, d_out, out_stride, st),
+            "disp_to_msg");
+    return SGM_OK;
+}
+
+void sgm_calc_q(const double K[9], const double Pr[12], const double Pl[12], double Q[16])
+{
+    // disparity_to_depth.cpp:62-84
+    const double cx = Pl[2], cxr = Pr[2], cy = Pl[4 + 2], fx = K[0];
+    const double p14 = Pr[3];
+    const double T = -p14 / fx;
+    const double q33 = -(cx - cxr) / T;
+    for (int i = 0; i < 16; i++) Q[i] = 0.0;
+    Q[0] = 1.0;  Q[3] = -cx;
+    Q[5] = 1.0;  Q[7] = -cy;
+    Q[11] = fx;
+    Q[14] = 1.0 / T;
+    Q[15] = q33;
+}
+
+int sgm_depth_points(sgm_handle* h, const float* d_disp, size_t disp_stride, int W, int H, const uint8_t* d_color,
+                     size_t color_stride, int channels, const double q[5], double depth_min, double depth_max,
+                     float* d_depth, size_t depth_stride, sgm_point_xyzrgb* d_points, int max_points,
+                     int* d_num_points, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!d_disp || !q || W <= 0 || H <= 0 || disp_stride < (size_t)W || (d_depth && depth_stride < (size_t)W) ||
+        (channels != 0 && channels != 1 && channels != 3) || (channels && !d_color) ||
+        (channels && color_stride < (size_t)W * channels) || (d_points && max_points < 0))
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    if (h->aux_n < (size_t)(2 * H + 1)) {
+        if (h->aux) (void)hipFree(h->aux);
+        h->aux = nullptr;
+        h->aux_n = 0;
+        HIP_TRY(hipMalloc(&h->aux, sizeof(int) * (2 * (size_t)H + 1)), "hipMalloc aux");
+        h->aux_n = 2 * (size_t)H + 1;
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const float qf[5] = {(float)q[0], (float)q[1], (float)q[2], (float)q[3], (float)q[4]};   // :134-138
+    int* row_count = h->aux;
+    int* row_off = h->aux + H;
+    HIP_TRY(sgm::launch_depth_points(d_disp, disp_stride, W, H, qf, depth_min, depth_max, d_color, color_stride,
+                                     channels, d_depth, depth_stride, (float4*)d_points, d_points ? max_points : 0,
+                                     row_count, row_off, st), "depth_points");
+    if (d_num_points)
+        HIP_TRY(hipMemcpyAsync(d_num_points, row_off + H, sizeof(int), hipMemcpyDeviceToDevice, st), "count");
+    return SGM_OK;
 }
 
 int sgm_synchronize(sgm_handle* h)

@@ -143,6 +143,36 @@ double sgm_stage_bytes(const sgm_handle* h, int i);
 /* Number of launches of stage i recorded since profiling was enabled.                    */
 int  sgm_stage_launches(const sgm_handle* h, int i);
 
+/* ---- after the matcher: DisparityImage packing and disparity -> depth / point cloud ----- */
+/* The node's processDisparity tail (generate_disparity.cpp:426-452) on device buffers:
+ * out = disp * (1/16) as float, then MISSING_Z (10000) where out < min_disparity and where
+ * out > max_disparity (min/max = T*f/depth_max and T*f/depth_min, as float, :447-450).
+ * Asynchronous on `stream` (NULL = the handle's stream).                                   */
+int  sgm_disparity_to_msg(sgm_handle* h, const int16_t* d_disp, size_t disp_stride, int width, int height,
+                          float min_disparity, float max_disparity, float* d_out, size_t out_stride,
+                          void* stream);
+
+/* Q of disparity_to_depth.cpp calc_q (:62-84) from the left camera matrix K (3x3) and the
+ * rectified projections P_right, P_left (3x4), all row-major doubles. Host-only.          */
+void sgm_calc_q(const double K_left[9], const double P_right[12], const double P_left[12], double Q[16]);
+
+/* One point of the cloud: pcl::PointXYZRGB's x, y, z and its packed rgba (b | g<<8 | r<<16 |
+ * 255<<24).                                                                                 */
+typedef struct sgm_point_xyzrgb { float x, y, z; uint32_t rgba; } sgm_point_xyzrgb;
+
+/* disparity_to_depth.cpp:127-205 on device buffers, asynchronous on `stream`:
+ *   d_disp     DisparityImage float image (pixels; 0 and MISSING_Z are skipped)
+ *   d_color    MONO8 (channels 1) / BGR8 (channels 3) image, or NULL with channels 0 (black)
+ *   q          {Q(2,3), Q(0,3), Q(1,3), Q(3,2), Q(3,3)} (cast to float, as the node does)
+ *   depth_min/max  the node's depth window (z kept when depth_min <= z <= depth_max)
+ *   d_depth    (may be NULL) W x H float depth, 0 where no point
+ *   d_points   (may be NULL) the first max_points points in raster order (pcl push_back order)
+ *   d_num_points (device int, may be NULL) receives the total number of points.           */
+int  sgm_depth_points(sgm_handle* h, const float* d_disp, size_t disp_stride, int width, int height,
+                      const uint8_t* d_color, size_t color_stride, int channels, const double q[5],
+                      double depth_min, double depth_max, float* d_depth, size_t depth_stride,
+                      sgm_point_xyzrgb* d_points, int max_points, int* d_num_points, void* stream);
+
 /* ---- stage entry points (parity tests compare each stage with the CPU oracle) ----------- */
 /* 9x7 census codes of one image (host buffers; out: W x H uint64, row-major).             */
 int  sgm_debug_census(sgm_handle* h, const uint8_t* img, int width, int height,

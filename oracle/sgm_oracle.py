@@ -186,3 +186,74 @@ def set_threads(n):
 
 def num_threads():
     return int(lib().sgmref_num_threads())
+
+
+# ---------------------------------------------------------------------------------------
+# After the matcher: numpy float32 restatements. numpy applies
+# one IEEE rounding per float32 operation (no fused multiply-add), the same as the
+# reference's scalar C++ expressions; parity with the GPU is bit-exact.
+# ---------------------------------------------------------------------------------------
+MISSING_Z = np.float32(10000.0)      # image_geometry::StereoCameraModel::MISSING_Z
+
+
+def disparity_to_msg(disp16, min_disparity, max_disparity):
+    """generate_disparity.cpp:426-452: convertTo(dmat, CV_32F, 1/16), then
+    setTo(MISSING_Z, dmat < min_disparity) and setTo(MISSING_Z, dmat > max_disparity)."""
+    d = np.asarray(disp16, np.int16).astype(np.float32) * np.float32(0.0625)
+    d[d < np.float32(min_disparity)] = MISSING_Z
+    d[d > np.float32(max_disparity)] = MISSING_Z
+    return d
+
+
+def calc_q(K, P_right, P_left):
+    """disparity_to_depth.cpp:62-84 (doubles)."""
+    K = np.asarray(K, np.float64).reshape(3, 3)
+    Pr = np.asarray(P_right, np.float64).reshape(3, 4)
+    Pl = np.asarray(P_left, np.float64).reshape(3, 4)
+    cx, cxr, cy, fx = Pl[0, 2], Pr[0, 2], Pl[1, 2], K[0, 0]
+    T = -Pr[0, 3] / fx
+    q = np.zeros((4, 4), np.float64)
+    q[0, 0] = 1.0
+    q[0, 3] = -cx
+    q[1, 1] = 1.0
+    q[1, 3] = -cy
+    q[2, 3] = fx
+    q[3, 2] = 1.0 / T
+    q[3, 3] = -(cx - cxr) / T
+    return q
+
+
+def depth_points(disp, Q, depth_min, depth_max, color=None):
+    """disparity_to_depth.cpp:127-205: depth image and the XYZRGB points in push_back
+    (raster) order. Q(2,3), Q(0,3), Q(1,3), Q(3,2), Q(3,3) are cast to float (:134-138); the
+    depth window is compared in double (z promoted). color: None, HxW (MONO8) or HxWx3 (BGR8).
+    Returns (depth float32 HxW, points float32 Nx3, rgba uint32 N)."""
+    d = np.asarray(disp, np.float32)
+    h, w = d.shape
+    Q = np.asarray(Q, np.float64)
+    wz, q03, q13, q32, q33 = (np.float32(Q[2, 3]), np.float32(Q[0, 3]), np.float32(Q[1, 3]),
+                              np.float32(Q[3, 2]), np.float32(Q[3, 3]))
+    jj = np.broadcast_to(np.arange(w, dtype=np.float32)[None, :], (h, w))
+    ii = np.broadcast_to(np.arange(h, dtype=np.float32)[:, None], (h, w))
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        ww = d * q32 + q33                      # two float32 roundings, like the C++ expression
+        x = (jj + q03) / ww
+        y = (ii + q13) / ww
+        z = wz / ww
+        ok = (d != 0) & (d != MISSING_Z) & (ww > 0) & (z > 0)
+        z64 = z.astype(np.float64)
+        ok &= (z64 <= float(depth_max)) & (z64 >= float(depth_min))
+    depth = np.where(ok, z, np.float32(0)).astype(np.float32)
+    sel = np.nonzero(ok.ravel())[0]
+    pts = np.stack([x.ravel()[sel], y.ravel()[sel], z.ravel()[sel]], axis=1).astype(np.float32)
+    if color is None:
+        b = g = r = np.zeros(len(sel), np.uint32)
+    else:
+        c = np.asarray(color, np.uint8)
+        if c.ndim == 2:
+            b = g = r = c.ravel()[sel].astype(np.uint32)
+        else:
+            cc = c.reshape(-1, 3)[sel].astype(np.uint32)
+            b, g, r = cc[:, 0], cc[:, 1], cc[:, 2]
+    rgba = (np.uint32(0xFF000000) | (r << 16) | (g << 8) | b).astype(np.uint32)
+    return depth, pts, rgba
