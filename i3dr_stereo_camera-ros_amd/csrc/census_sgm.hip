@@ -352,8 +352,9 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     bool pv = false;
     const bool lane_act = EXACT || p * DPL < g.D;
     const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
-    // stores: 32-bit offsets from the wave-uniform volume base (cells or the trash slot)
-    const uint32_t tr_off = (uint32_t)(trash - V) + (uint32_t)((tid & 63) * DPL);
+    // stores: the step's row base is wave-uniform (64-bit, scalar math); lanes add a 32-bit
+    // offset inside the row (< width1 * D), or go to their trash slot
+    uint8_t* const tr = trash + (tid & 63) * DPL;
     const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
 
     // Segments are staged in LDS (double buffer, one barrier per step) from registers loaded
@@ -380,9 +381,9 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         const uint32_t P2x = pv ? P2P2 : kBaseP2;
         p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
         const bool ok = valid && lane_act;
-        const uint32_t off = ok
-            ? (uint32_t)((min(max(y, 0), g.H - 1) * g.width1 + (x - g.minX1)) * g.D + p * DPL) : tr_off;
-        store_pairs<DPL>(V + off, V + ((ok && hi_ok) ? off + 16 : tr_off + 16), Labs);
+        uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
+        uint8_t* const dst = ok ? vrow + (uint32_t)((x - g.minX1) * g.D + p * DPL) : tr;
+        store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
         pv = valid;
     };
     // step s reads buf[s & 1] (holding segment s), then segment s + 1 (register set
@@ -480,15 +481,17 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     const int r = lane >> 4, p = lane & 15;
     R.init(g, tid, kWG);
     const bool lane_act = EXACT || p * DPL < g.D;
-    // 32-bit offsets from wave-uniform volume bases: SGPR-base + VGPR-offset addressing
-    const uint32_t off0 = (uint32_t)(y * g.width1 * g.D) + (lane_act ? p * DPL : 0);
+    // wave-uniform 64-bit volume row base (a C5 volume is 5.5 GB) + 32-bit lane offsets:
+    // SGPR-base + VGPR-offset addressing
+    const size_t row0 = (size_t)y * g.width1 * g.D;
+    const uint32_t off0 = (uint32_t)(lane_act ? p * DPL : 0);
     uint32_t* srow = sl + (w * 4 + r) * 8 * DPL;
     const int n = g.width1;
     const int nq = (n + 3) / 4;
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
         const uint32_t off = off0 + (uint32_t)(min(4 * q + r, n - 1) * g.D);
 #pragma unroll
-        for (int vv = 0; vv < 8; vv++) wload<DPL>(vols + (size_t)vv * vol_bytes + off, v[vv]);
+        for (int vv = 0; vv < 8; vv++) wload<DPL>(vols + (size_t)vv * vol_bytes + row0 + off, v[vv]);
     };
     uint32_t cur[8][NWD], nxt[8][NWD];
     load(min(w, nq - 1), cur);

@@ -710,11 +710,12 @@ int sgm_match(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, s
     return SGM_OK;
 }
 
-int sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights, int n_frames, int W,
-                    int H, size_t stride, int16_t* const* disps, size_t out_stride, const int* devices, int n_dev)
+}  // extern "C"
+
+// Per-device sub-handles (created on demand, parameters copied from h); devs = the devices.
+static int open_subs(sgm_handle* h, const int* devices, int n_dev, std::vector<int>& devs)
 {
-    if (!h || !lefts || !rights || !disps || n_frames < 0) return SGM_ERR_ARG;
-    std::vector<int> devs;
+    devs.clear();
     if (!devices || n_dev <= 0) {
         const int n = sgm_device_count();
         for (int i = 0; i < n; i++) devs.push_back(i);
@@ -722,32 +723,77 @@ int sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* c
         devs.assign(devices, devices + n_dev);
     }
     if (devs.empty()) return fail(h, SGM_ERR_DEVICE, "no HIP device");
-    {
-        std::lock_guard<std::mutex> lk(h->mu);
-        while (h->sub.size() < devs.size()) h->sub.push_back(nullptr);
-        for (size_t i = 0; i < devs.size(); i++) {
-            if (h->sub[i] && h->sub[i]->device != devs[i]) { sgm_destroy(h->sub[i]); h->sub[i] = nullptr; }
-            if (!h->sub[i]) {
-                int rc = sgm_create(&h->sub[i], devs[i]);
-                if (rc) return fail(h, rc, "cannot open device " + std::to_string(devs[i]));
-            }
-            h->sub[i]->params = h->params;
+    std::lock_guard<std::mutex> lk(h->mu);
+    while (h->sub.size() < devs.size()) h->sub.push_back(nullptr);
+    for (size_t i = 0; i < devs.size(); i++) {
+        if (h->sub[i] && h->sub[i]->device != devs[i]) { sgm_destroy(h->sub[i]); h->sub[i] = nullptr; }
+        if (!h->sub[i]) {
+            int rc = sgm_create(&h->sub[i], devs[i]);
+            if (rc) return fail(h, rc, "cannot open device " + std::to_string(devs[i]));
         }
+        h->sub[i]->params = h->params;
     }
+    return SGM_OK;
+}
+
+// Runs job(t, sub-handle) on one host thread per device; first error wins.
+template <typename F>
+static int run_on_subs(sgm_handle* h, const std::vector<int>& devs, F job)
+{
     std::vector<int> rcs(devs.size(), SGM_OK);
     std::vector<std::thread> th;
-    for (size_t t = 0; t < devs.size(); t++) {
-        th.emplace_back([&, t]() {
-            for (int i = (int)t; i < n_frames; i += (int)devs.size()) {
-                int rc = sgm_match(h->sub[t], lefts[i], rights[i], W, H, stride, disps[i], out_stride);
-                if (rc) { rcs[t] = rc; return; }
-            }
-        });
-    }
+    for (size_t t = 0; t < devs.size(); t++) th.emplace_back([&, t]() { rcs[t] = job((int)t, h->sub[t]); });
     for (auto& t : th) t.join();
     for (size_t t = 0; t < devs.size(); t++)
         if (rcs[t]) return fail(h, rcs[t], std::string("device ") + std::to_string(devs[t]) + ": " + h->sub[t]->err);
     return SGM_OK;
+}
+
+extern "C" {
+
+int sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights, int n_frames, int W,
+                    int H, size_t stride, int16_t* const* disps, size_t out_stride, const int* devices, int n_dev)
+{
+    if (!h || !lefts || !rights || !disps || n_frames < 0) return SGM_ERR_ARG;
+    std::vector<int> devs;
+    int rc = open_subs(h, devices, n_dev, devs);
+    if (rc) return rc;
+    const int nd = (int)devs.size();
+    return run_on_subs(h, devs, [&](int t, sgm_handle* sub) {
+        for (int i = t; i < n_frames; i += nd) {
+            int r = sgm_match(sub, lefts[i], rights[i], W, H, stride, disps[i], out_stride);
+            if (r) return r;
+        }
+        return (int)SGM_OK;
+    });
+}
+
+int sgm_match_tiled(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int16_t* disp,
+                    size_t out_stride, int n_bands, int halo, const int* devices, int n_dev)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W || n_bands < 1 ||
+        halo < 0)
+        return fail(h, SGM_ERR_ARG, "bad buffers, sizes, band count or halo");
+    n_bands = std::min(n_bands, H);
+    std::vector<int> devs;
+    int rc = open_subs(h, devices, n_dev, devs);
+    if (rc) return rc;
+    const int nd = (int)devs.size();
+    return run_on_subs(h, devs, [&](int t, sgm_handle* sub) {
+        std::vector<int16_t> band;
+        for (int b = t; b < n_bands; b += nd) {
+            const int c0 = (int)((long long)b * H / n_bands), c1 = (int)((long long)(b + 1) * H / n_bands);
+            const int e0 = std::max(0, c0 - halo), e1 = std::min(H, c1 + halo);
+            band.resize((size_t)W * (e1 - e0));
+            int r = sgm_match(sub, L + (size_t)e0 * stride, R + (size_t)e0 * stride, W, e1 - e0, stride, band.data(),
+                              (size_t)W);
+            if (r) return r;
+            for (int y = c0; y < c1; y++)
+                std::memcpy(disp + (size_t)y * out_stride, band.data() + (size_t)(y - e0) * W, sizeof(int16_t) * W);
+        }
+        return (int)SGM_OK;
+    });
 }
 
 int sgm_set_profiling(sgm_handle* h, int enable)

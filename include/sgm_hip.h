@@ -114,6 +114,15 @@ int  sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* 
                      int16_t* const* disps, size_t out_stride,
                      const int* devices, int n_dev);
 
+/* One large frame split into n_bands row bands (band b -> devices[b % n_dev]), SURVEY §8(e)
+ * "single huge frame" in overlap mode: each band is matched on its rows extended by `halo`
+ * rows above and below, and only its own rows are kept. No path state crosses bands, so
+ * pixels near band seams can differ from the full-frame result (the tests report the
+ * disagreement); n_bands = 1 is exactly sgm_match. Host buffers; synchronous.          */
+int  sgm_match_tiled(sgm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                     size_t stride, int16_t* disp, size_t out_stride, int n_bands, int halo,
+                     const int* devices, int n_dev);
+
 /* Frame batch on device buffers (host arrays of n_frames device pointers), asynchronous on
  * `stream`. Census mode pipelines the frames: the path aggregation of frame i+1 and the
  * WTA of frame i run in ONE launch (VALU-bound and HBM-bound work side by side), with two

@@ -217,3 +217,48 @@ def test_device_batch_pipeline(engine, oracle, pkg, synth, kw, n):
         ng = (n + 1) // 2
         assert launches["paths8"] == 1 and launches["wta_lr"] == 1
         assert launches.get("paths8+wta_lr", 0) == ng - 1
+
+
+def test_tiled_single_band_is_exact(engine, oracle, synth, pkg):
+    """sgm_match_tiled with one band is the full-frame match."""
+    left, right, _ = synth.stereo_pair(96, 256, 0, 64, seed=41)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    assert np.array_equal(engine.match_tiled(left, right, 1, 0), oracle.match(to_oracle_params(oracle, p), left, right))
+
+
+@pytest.mark.parametrize("bands,halo", [(4, 0), (4, 16), (4, 64), (8, 128)])
+def test_tiled_overlap_mode_disagreement(engine, oracle, synth, pkg, bands, halo):
+    """SURVEY §8(e) C5 overlap mode: row bands with halos, no path-state exchange. Each band
+    equals the oracle run on its extended rows (exact), and the disagreement with the
+    full-frame result shrinks as the halo grows (reported)."""
+    h, w, D = 384, 448, 128
+    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=43)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D)
+    engine.set_params(p)
+    got = engine.match_tiled(left, right, bands, halo)
+    op = to_oracle_params(oracle, p)
+    for b in range(bands):
+        c0, c1 = b * h // bands, (b + 1) * h // bands
+        e0, e1 = max(0, c0 - halo), min(h, c1 + halo)
+        ref = oracle.match(op, left[e0:e1], right[e0:e1])
+        assert np.array_equal(got[c0:c1], ref[c0 - e0:c1 - e0]), f"band {b}"
+    full = oracle.match(op, left, right)
+    frac = float((got != full).mean())
+    print(f"bands={bands} halo={halo}: {100 * frac:.3f} % of pixels differ from the full-frame match")
+    assert frac < {0: 0.1, 16: 0.01, 64: 0.001, 128: 0.001}[halo]
+
+
+def test_c5_tiled_vs_full_frame(engine, synth, pkg):
+    """BASELINE config C5 (4096x3000, D=512, 8-path + subpixel + LR): 8 row bands with a
+    128-row halo (the 8-GPU layout, run here on the visible devices) against the
+    single-device full frame (44 GB of path volumes, resident in HBM)."""
+    h, w, D = 3000, 4096, 512
+    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=5, with_truth=False)
+    engine.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D))
+    full = engine.match(left, right)
+    tiled = engine.match_tiled(left, right, 8, 128)
+    frac = float((tiled != full).mean())
+    print(f"C5 8 bands, halo 128: {100 * frac:.4f} % of pixels differ from the full frame")
+    assert frac < 0.001
+    assert (full != -16).mean() > 0.5
