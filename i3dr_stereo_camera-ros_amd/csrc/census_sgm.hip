@@ -586,15 +586,60 @@ __global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_b
 // the CUs the path sweeps' tail leaves idle (measured at C3 for one frame: WTA first
 // 2.02 ms, interleaved 1.97, evenly from 30 % 1.92, last 1.71).
 // ------------------------------------------------------------------------------------
+// Census of the next group in the same launch: 64 x 32 pixel blocks (a 38 x 72 byte LDS
+// tile, 8 pixels per thread), dispatched after every path and WTA block, so they run in
+// the tail where CUs idle. Images are blocks [0, 2n): frame i left = 2i, right = 2i+1.
+constexpr int kCensusRows = 32;
+
+__device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int H, int b, uint8_t* tile)
+{
+    const int bx = (W + 63) / 64, per_img = bx * ((H + kCensusRows - 1) / kCensusRows);
+    const int img = b / per_img, r = b - img * per_img;
+    const int f = img >> 1, by = r / bx;
+    const uint8_t* src = (img & 1) ? pick4(cf.R, f) : pick4(cf.L, f);
+    uint64_t* out = (img & 1) ? pick4(cf.cR, f) : pick4(cf.cL, f);
+    const int x0 = (r - by * bx) * 64, y0 = by * kCensusRows;
+    constexpr int TH = kCensusRows + 6;
+    for (int i = threadIdx.x; i < TH * 72; i += kWG) {
+        const int ty = i / 72, tx = i - ty * 72;
+        const int yy = min(max(y0 + ty - 3, 0), H - 1), xx = min(max(x0 + tx - 4, 0), W - 1);
+        tile[i] = src[(size_t)yy * cf.stride + xx];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 63, x = x0 + tx;
+    if (x >= W) return;
+    for (int ty = threadIdx.x >> 6; ty < kCensusRows; ty += kWG / 64) {
+        const int y = y0 + ty;
+        if (y >= H) break;
+        const uint8_t* t0 = tile + ty * 72 + tx;
+        const int c = t0[3 * 72 + 4];
+        uint64_t code = 0;
+        int bit = 0;
+#pragma unroll
+        for (int dy = 0; dy < 7; dy++) {
+#pragma unroll
+            for (int dx = 0; dx < 9; dx++) {
+                if (dy == 3 && dx == 4) continue;
+                code |= (uint64_t)(t0[dy * 72 + dx] < c) << bit;
+                bit++;
+            }
+        }
+        out[(size_t)y * W + x] = code;
+    }
+}
+
+// blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf
 template <int DPL, bool EXACT>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
-void k_census_fused16(PathFrames pf, WtaFrames wf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                      const uint32_t* __restrict__ items, int n_items, size_t out_stride)
+void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_bytes, size_t trash_off, Geom g,
+                      PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride)
 {
     extern __shared__ uint64_t lds_dyn64[];
     const int b = blockIdx.x;
-    if (b >= n_items) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, b - n_items, (uint32_t*)lds_dyn64);
-    else paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64);
+    const int n_wta = g.H * wf.n;
+    if (b < n_items) paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64);
+    else if (b < n_items + n_wta) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, b - n_items, (uint32_t*)lds_dyn64);
+    else census_block(cf, g.W, g.H, b - n_items - n_wta, (uint8_t*)lds_dyn64);
 }
 
 // ------------------------------------------------------------------------------------
@@ -737,33 +782,36 @@ hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& 
 }
 
 template <int DPL>
-static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, size_t trash_off,
-                             const Geom& g, const PathLaunch16& pl, const uint32_t* items, int n_items,
-                             size_t out_stride, hipStream_t st)
+static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const CensusFrames& cf, size_t vol_bytes,
+                             size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
+                             int n_items, size_t out_stride, hipStream_t st)
 {
-    dim3 grid(n_items + g.H * wf.n), block(kWG);
-    const size_t lds = std::max(wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF);
+    const int n_census = ((g.W + 63) / 64) * ((g.H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
+    dim3 grid(n_items + g.H * wf.n + n_census), block(kWG);
+    const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF,
+                                 (size_t)(kCensusRows + 6) * 72});
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride);
+        hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
+                           pl, items, n_items, out_stride);
     else
-        hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride);
+        hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
+                           pl, items, n_items, out_stride);
 }
 
-// Path sweeps of the frames in pf fused with the WTA of the frames in wf (the previous
-// group). All volume sets have the same geometry.
-hipError_t launch_census_fused(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, const Geom& g,
-                               const uint32_t* items, int n_items, size_t out_stride, hipStream_t st)
+// One launch: path sweeps of the frames in pf (items), WTA of the frames in wf (the previous
+// group) and census of the frames in cf (the next group). Any of the three may be empty
+// (n_items = 0, wf.n = 0, cf.n = 0). All volume sets have the same geometry.
+hipError_t launch_census_fused(const PathFrames& pf, const WtaFrames& wf, const CensusFrames& cf, size_t vol_bytes,
+                               const Geom& g, const uint32_t* items, int n_items, size_t out_stride, hipStream_t st)
 {
     const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
-    case 2: launch_fused_dpl<2>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 4: launch_fused_dpl<4>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 8: launch_fused_dpl<8>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 16: launch_fused_dpl<16>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    default: launch_fused_dpl<32>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 2: launch_fused_dpl<2>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 4: launch_fused_dpl<4>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 8: launch_fused_dpl<8>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 16: launch_fused_dpl<16>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    default: launch_fused_dpl<32>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
     }
     return hipGetLastError();
 }

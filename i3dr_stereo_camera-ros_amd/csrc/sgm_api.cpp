@@ -25,7 +25,8 @@ hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint6
 int census_path_items(const Geom&, int, int, int, uint32_t*, int);
 hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t);
 hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
-hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, size_t, const Geom&, const uint32_t*, int, size_t,
+hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
+                               const uint32_t*, int, size_t,
                                hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
@@ -395,9 +396,12 @@ int batch_group(int n)
 }
 
 // Census-mode frame pipeline on h->stream, in groups of l.group frames (sets 2*group):
-//   census(G0) paths(G0) | census(Gk) fused[paths(Gk) + wta(Gk-1)] post(Gk-1) ... | wta(Glast) post
-// With a median the WTA of a group writes each frame's raw disparity to its own scratch
-// image (post filters read it), so no frame's output is overwritten before its median.
+//   census(G0) | fused[paths(G0) + census(G1)] | fused[paths(Gk) + wta(Gk-1) + census(Gk+1)] post(Gk-1)
+//   ... | wta(Glast) post
+// The census of group k+1 writes the code set of group k-1, whose path sweeps finished in
+// the previous launch. With a median the WTA of a group writes each frame's raw disparity
+// to its own scratch image (post filters read it), so no frame's output is overwritten
+// before its median.
 int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* const* dLs,
                      const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride)
 {
@@ -436,26 +440,39 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         }
         return wf;
     };
-    for (int k = 0; k <= ng; k++) {
-        if (k < ng) {
-            for (int f = 0; f < frames_of(k); f++) {
-                const int set = (k & 1) * G + f;
-                rec.begin("census", 2 * WH + 16 * WH);
-                HIP_TRY(sgm::launch_census(dLs[k * G + f], dRs[k * G + f], stride, g.W, g.H,
-                                           (uint64_t*)(ws + l.cL[set]), (uint64_t*)(ws + l.cR[set]), st),
-                        "census");
-            }
+    auto census_frames = [&](int k) {
+        sgm::CensusFrames cf{};
+        cf.n = frames_of(k);
+        cf.stride = stride;
+        for (int f = 0; f < cf.n; f++) {
+            const int set = (k & 1) * G + f;
+            cf.L[f] = dLs[k * G + f];
+            cf.R[f] = dRs[k * G + f];
+            cf.cL[f] = (uint64_t*)(ws + l.cL[set]);
+            cf.cR[f] = (uint64_t*)(ws + l.cR[set]);
         }
-        if (k == 0) {
-            rec.begin("paths8", 8 * cells * frames_of(0));
-            HIP_TRY(sgm::launch_census_paths(path_frames(0), l.vol_bytes, g, items, n_items, st), "paths");
-        } else if (k < ng) {
-            rec.begin("paths8+wta_lr", (16 * cells + 2 * WH) * G);
-            HIP_TRY(sgm::launch_census_fused(path_frames(k), wta_frames(k - 1), l.vol_bytes, g, items, n_items,
-                                             dst_stride, st), "fused");
-        } else {
+        return cf;
+    };
+    for (int f = 0; f < frames_of(0); f++) {
+        rec.begin("census", 2 * WH + 16 * WH);
+        HIP_TRY(sgm::launch_census(dLs[f], dRs[f], stride, g.W, g.H, (uint64_t*)(ws + l.cL[f]),
+                                   (uint64_t*)(ws + l.cR[f]), st), "census");
+    }
+    for (int k = 0; k <= ng; k++) {
+        if (k == ng) {
             rec.begin("wta_lr", (8 * cells + 2 * WH) * frames_of(k - 1));
             HIP_TRY(sgm::launch_census_wta(wta_frames(k - 1), l.vol_bytes, g, dst_stride, st), "wta");
+        } else if (ng == 1) {
+            rec.begin("paths8", 8 * cells * frames_of(0));
+            HIP_TRY(sgm::launch_census_paths(path_frames(0), l.vol_bytes, g, items, n_items, st), "paths");
+        } else {
+            const sgm::WtaFrames wf = k > 0 ? wta_frames(k - 1) : sgm::WtaFrames{};
+            const sgm::CensusFrames cf = k + 1 < ng ? census_frames(k + 1) : sgm::CensusFrames{};
+            // stage name and algorithmic bytes from the parts this launch carries
+            const char* name = wf.n ? (cf.n ? "paths8+wta_lr+census" : "paths8+wta_lr") : "paths8+census";
+            rec.begin(name, 8 * cells * frames_of(k) + (8 * cells + 2 * WH) * wf.n + 18 * WH * cf.n);
+            HIP_TRY(sgm::launch_census_fused(path_frames(k), wf, cf, l.vol_bytes, g, items, n_items, dst_stride, st),
+                    "fused");
         }
         if (k > 0) {
             const int k1 = k - 1;

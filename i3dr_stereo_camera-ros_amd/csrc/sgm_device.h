@@ -233,6 +233,15 @@ struct WtaFrames {
     int16_t* out[kMaxGroup];
     int n;
 };
+// census transforms of the next group, run in the tail of a fused launch
+struct CensusFrames {
+    const uint8_t* L[kMaxGroup];
+    const uint8_t* R[kMaxGroup];
+    uint64_t* cL[kMaxGroup];
+    uint64_t* cR[kMaxGroup];
+    size_t stride;
+    int n;
+};
 
 struct RowLds {
     uint32_t* key; int16_t* drow; int16_t* bst; uint16_t* mins;

@@ -212,11 +212,15 @@ def test_device_batch_pipeline(engine, oracle, pkg, synth, kw, n):
     for i, (l, r, _) in enumerate(frames):
         ref = oracle.match(op, l, r)
         assert np.array_equal(got[i], ref), f"frame {i}: {(got[i] != ref).sum()} pixels differ"
-    assert launches["census"] == n
-    if n >= 2:      # groups of (default) 2 frames: paths(G0) | fused[paths(Gk) + wta(Gk-1)] ... | wta(Glast)
-        ng = (n + 1) // 2
-        assert launches["paths8"] == 1 and launches["wta_lr"] == 1
-        assert launches.get("paths8+wta_lr", 0) == ng - 1
+    # groups of (default) 2 frames: census(G0) | fused[paths(G0) + census(G1)] |
+    # fused[paths(Gk) + wta(Gk-1) + census(Gk+1)] ... | fused[paths(Glast) + wta] | wta(Glast)
+    ng = (n + 1) // 2
+    assert launches["census"] == min(n, 2) and launches["wta_lr"] == 1
+    if ng == 1:
+        assert launches["paths8"] == 1
+    else:
+        assert launches["paths8+census"] == 1 and launches["paths8+wta_lr"] == 1
+        assert launches.get("paths8+wta_lr+census", 0) == ng - 2
 
 
 def test_tiled_single_band_is_exact(engine, oracle, synth, pkg):

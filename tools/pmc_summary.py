@@ -13,7 +13,7 @@ import csv
 import glob
 import json
 
-STAGE_OF = {"k_census9x7": "census", "k_census_paths16": "paths8", "k_census_wta16": "wta_lr", "k_census_fused16": "paths8+wta_lr",
+STAGE_OF = {"k_census9x7": "census", "k_census_paths16": "paths8", "k_census_wta16": "wta_lr", "k_census_fused16": "fused",
             "k_ocv_pixcost": "ocv_cost", "k_ocv_paths": "ocv_paths", "k_ocv_wta": "ocv_wta_lr"}
 
 
