@@ -421,6 +421,17 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
 }
 
+// SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
+// HW_ID, start, end} (s_memrealtime, 100 MHz)
+__device__ __forceinline__ void trace_record(uint64_t* trace, uint64_t tag, uint64_t t0)
+{
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
+    uint64_t* r = trace + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+    r[0] = tag | ((uint64_t)blockIdx.x << 32); r[1] = ((uint64_t)xcc << 32) | hw; r[2] = t0; r[3] = t1;
+}
+
 template <int DPL, bool EXACT>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
 void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
@@ -429,13 +440,8 @@ void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g,
     __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
-    if (trace && (threadIdx.x & 63) == 0) {        // debug timeline (SGM_TRACE): one record per wave
-        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
-        uint64_t* r = trace + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
-        r[0] = items[blockIdx.x] | ((uint64_t)blockIdx.x << 32); r[1] = ((uint64_t)xcc << 32) | hw; r[2] = t0; r[3] = t1;
-    }
+    if (trace && (threadIdx.x & 63) == 0)        // debug timeline (SGM_TRACE): one record per wave
+        trace_record(trace, items[blockIdx.x], t0);
 }
 
 // ====================================================================================
@@ -632,14 +638,31 @@ __device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int 
 template <int DPL, bool EXACT>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
 void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_bytes, size_t trash_off, Geom g,
-                      PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride)
+                      PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride,
+                      int period16, uint64_t* __restrict__ trace)
 {
     extern __shared__ uint64_t lds_dyn64[];
+    const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const int b = blockIdx.x;
     const int n_wta = g.H * wf.n;
-    if (b < n_items) paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64);
-    else if (b < n_items + n_wta) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, b - n_items, (uint32_t*)lds_dyn64);
-    else census_block(cf, g.W, g.H, b - n_items - n_wta, (uint8_t*)lds_dyn64);
+    // paths and WTA blocks merged: among the first b+1 blocks, wcount(b) are WTA rows
+    // (one in period16/16 blocks, period16 = 0: all WTA rows after the paths)
+    auto wcount = [&](int bb) {
+        int w = period16 > 0 ? min((bb + 1) * 16 / period16, n_wta) : 0;
+        return max(w, bb + 1 - n_items);
+    };
+    int kind = 2, idx = b - n_items - n_wta;
+    if (b < n_items + n_wta) {
+        const int w = wcount(b);
+        const bool is_wta = w > (b > 0 ? wcount(b - 1) : 0);
+        kind = is_wta ? 1 : 0;
+        idx = is_wta ? w - 1 : b - w;
+    }
+    if (kind == 0) paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[idx], lds_dyn64);
+    else if (kind == 1) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, idx, (uint32_t*)lds_dyn64);
+    else census_block(cf, g.W, g.H, idx, (uint8_t*)lds_dyn64);
+    if (trace && (threadIdx.x & 63) == 0)         // debug timeline (SGM_TRACE), kind in bits 62-63
+        trace_record(trace, (kind == 0 ? items[idx] : 0u) | ((uint64_t)kind << 62), t0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -707,21 +730,38 @@ int census_path_items(const Geom& g, int only_dir, int n_slots, int group, uint3
     return n;
 }
 
+// SGM_TRACE=<file>: debug timeline of path / fused launches (one record per wave), written
+// after a synchronise by trace_dump. Never set in production runs.
+static uint64_t* trace_buffer(int n_blocks)
+{
+    static uint64_t* trace = nullptr;
+    static size_t trace_n = 0;
+    if (!getenv("SGM_TRACE")) return nullptr;
+    if (trace_n < (size_t)n_blocks * 16) {
+        if (trace) (void)hipFree(trace);
+        trace_n = (size_t)n_blocks * 16;
+        if (hipMalloc(&trace, trace_n * 8) != hipSuccess) { trace = nullptr; trace_n = 0; }
+    }
+    if (trace) (void)hipMemset(trace, 0, (size_t)n_blocks * 16 * 8);
+    return trace;
+}
+
+static void trace_dump(uint64_t* tr, int n_blocks, hipStream_t st)
+{
+    if (!tr) return;
+    std::vector<uint64_t> h((size_t)n_blocks * 16);
+    if (hipStreamSynchronize(st) == hipSuccess &&
+        hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+        FILE* f = fopen(getenv("SGM_TRACE"), "wb");
+        if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
+    }
+}
+
 template <int DPL>
 static void launch_paths_dpl(const PathFrames& pf, size_t vol_bytes, size_t trash_off, const Geom& g,
                              const PathLaunch16& pl, const uint32_t* items, int n_items, hipStream_t st)
 {
-    // SGM_TRACE=<file>: debug timeline of the path launch (one record per wave), written
-    // after a synchronise. Never set in production runs.
-    static uint64_t* trace = nullptr;
-    static size_t trace_n = 0;
-    const char* tpath = getenv("SGM_TRACE");
-    if (tpath && trace_n < (size_t)n_items * 16) {
-        if (trace) (void)hipFree(trace);
-        trace_n = (size_t)n_items * 16;
-        if (hipMalloc(&trace, trace_n * 8) != hipSuccess) { trace = nullptr; trace_n = 0; }
-    }
-    uint64_t* tr = tpath ? trace : nullptr;
+    uint64_t* tr = trace_buffer(n_items);
     dim3 grid(n_items), block(kWG);
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_paths16<DPL, true>), grid, block, 0, st, pf, vol_bytes, trash_off, g, pl, items,
@@ -729,14 +769,7 @@ static void launch_paths_dpl(const PathFrames& pf, size_t vol_bytes, size_t tras
     else
         hipLaunchKernelGGL((k_census_paths16<DPL, false>), grid, block, 0, st, pf, vol_bytes, trash_off, g, pl, items,
                            tr);
-    if (tr) {
-        std::vector<uint64_t> h((size_t)n_items * 16);
-        if (hipStreamSynchronize(st) == hipSuccess &&
-            hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            FILE* f = fopen(tpath, "wb");
-            if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
-        }
-    }
+    trace_dump(tr, n_items, st);
 }
 
 // Path sweeps of the frames in pf (codes -> volumes). Each volume slice is vol_bytes long:
@@ -790,12 +823,18 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
     dim3 grid(n_items + g.H * wf.n + n_census), block(kWG);
     const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF,
                                  (size_t)(kCensusRows + 6) * 72});
+    uint64_t* tr = trace_buffer((int)grid.x);
+    // WTA rows interleaved one per 2.75 blocks (C3 sweep: after the paths 554 pairs/s, 1/2 498,
+    // 1/2.5 578, 1/2.75 580, 1/3 577, 1/3.5 574): the HBM-bound rows co-run with the
+    // VALU-bound sweeps on ~1 slot in 4 instead of waiting for the sweeps' tail
+    static const int period = getenv("SGM_WTA_PERIOD") ? (int)(16 * atof(getenv("SGM_WTA_PERIOD"))) : 44;
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
-                           pl, items, n_items, out_stride);
+                           pl, items, n_items, out_stride, period, tr);
     else
         hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
-                           pl, items, n_items, out_stride);
+                           pl, items, n_items, out_stride, period, tr);
+    trace_dump(tr, (int)grid.x, st);
 }
 
 // One launch: path sweeps of the frames in pf (items), WTA of the frames in wf (the previous
