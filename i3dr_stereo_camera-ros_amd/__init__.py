@@ -41,7 +41,8 @@ EXPORTS = [
     "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
     "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
-    "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_debug_census",
+    "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
+    "sgm_remap_cubic", "sgm_cubic_table", "sgm_debug_census",
     "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
 ]
 
@@ -117,6 +118,11 @@ def load_library(path=None):
     L.sgm_depth_points.argtypes = [vp, vp, sz, ci, ci, vp, sz, ci, P(ctypes.c_double), ctypes.c_double,
                                    ctypes.c_double, vp, sz, vp, ci, vp, vp]
     L.sgm_stage_bytes.restype = ctypes.c_double
+    L.sgm_rectify_map.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), ci, P(ctypes.c_double),
+                                  P(ctypes.c_double), ci, ci, vp, vp, sz, vp]
+    L.sgm_remap_cubic.argtypes = [vp, vp, sz, ci, ci, vp, vp, sz, ci, ci, vp, sz, vp]
+    L.sgm_cubic_table.argtypes = [vp]
+    L.sgm_cubic_table.restype = None
     L.sgm_debug_census.argtypes = [vp, vp, ci, ci, sz, vp]
     L.sgm_debug_census_path.argtypes = [vp, vp, vp, ci, ci, sz, ci, vp]
     L.sgm_debug_ocv_cost.argtypes = [vp, vp, vp, ci, ci, sz, vp]
@@ -300,6 +306,28 @@ class Engine:
                                               vp(d_depth), depth_stride, vp(d_points), max_points,
                                               vp(d_num_points), vp(stream) if stream else None))
 
+    def rectify_map(self, K, D, R, P, width, height, d_map_x, d_map_y, map_stride, stream=None):
+        """initUndistortRectifyMap(K, D, R, P, (width, height), CV_32FC1) into device float maps
+        (generate_disparity.cpp:379-380). R None = identity; D: 0/4/5/8/12 coefficients."""
+        dv = ctypes.c_double
+        k = (dv * 9)(*np.asarray(K, np.float64).ravel())
+        dd = np.asarray([] if D is None else D, np.float64).ravel()
+        darr = (dv * max(len(dd), 1))(*dd)
+        r = (dv * 9)(*np.asarray(R, np.float64).ravel()) if R is not None else None
+        pp = (dv * 12)(*np.asarray(P, np.float64).ravel())
+        vp = ctypes.c_void_p
+        self._check(self.lib.sgm_rectify_map(self.h, k, darr, len(dd), r, pp, width, height, vp(d_map_x),
+                                             vp(d_map_y), map_stride, vp(stream) if stream else None))
+
+    def remap_cubic(self, d_src, src_stride, src_w, src_h, d_map_x, d_map_y, map_stride, width, height, d_dst,
+                    dst_stride, stream=None):
+        """cv::remap(src, dst, map_x, map_y, INTER_CUBIC, BORDER_CONSTANT) on device buffers
+        (generate_disparity.cpp:383)."""
+        vp = ctypes.c_void_p
+        self._check(self.lib.sgm_remap_cubic(self.h, vp(d_src), src_stride, src_w, src_h, vp(d_map_x), vp(d_map_y),
+                                             map_stride, width, height, vp(d_dst), dst_stride,
+                                             vp(stream) if stream else None))
+
     def census(self, img):
         img = np.ascontiguousarray(img, np.uint8)
         h, w = img.shape
@@ -351,6 +379,45 @@ def calc_q(K, P_right, P_left):
     return np.array(q[:], np.float64).reshape(4, 4)
 
 
+def _side_stream(torch):
+    """A stream ordered after everything already queued on torch's current stream (the
+    library's NULL-stream argument means the handle's own stream, not torch's)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    return st
+
+
+def cubic_table():
+    """The INTER_CUBIC int16 weight table of the library (host code, no device needed)."""
+    lib = load_library()
+    t = np.empty((1024, 16), np.int16)
+    lib.sgm_cubic_table(t.ctypes.data_as(ctypes.c_void_p))
+    return t
+
+
+def rectify(engine, image, K, D, R, P, maps=None):
+    """The node's rectify(image, camera_info) (generate_disparity.cpp:370-386) on the GPU:
+    initUndistortRectifyMap + remap INTER_CUBIC / BORDER_CONSTANT. `maps` (map_x, map_y
+    device tensors from a previous call) skips the map computation — the map depends only
+    on the calibration. Returns (rectified u8 image as numpy, maps)."""
+    import torch
+    img = torch.as_tensor(np.ascontiguousarray(image, np.uint8)).cuda()
+    h, w = img.shape
+    if maps is None:
+        mx = torch.empty((h, w), dtype=torch.float32, device="cuda")
+        my = torch.empty((h, w), dtype=torch.float32, device="cuda")
+        maps = (mx, my)
+    out = torch.empty((h, w), dtype=torch.uint8, device="cuda")
+    stream = _side_stream(torch)
+    if len(maps) == 2:
+        engine.rectify_map(K, D, R, P, w, h, maps[0].data_ptr(), maps[1].data_ptr(), w, stream.cuda_stream)
+        maps = (maps[0], maps[1], True)
+    engine.remap_cubic(img.data_ptr(), w, w, h, maps[0].data_ptr(), maps[1].data_ptr(), w, w, h, out.data_ptr(), w,
+                       stream.cuda_stream)
+    stream.synchronize()
+    return out.cpu().numpy(), maps
+
+
 def q_terms(Q):
     """The five Q entries the depth node uses (disparity_to_depth.cpp:134-138)."""
     Q = np.asarray(Q, np.float64)
@@ -371,12 +438,12 @@ def disp_info_to_depth(engine, disp_image, color, Q, depth_min=0.0, depth_max=10
     depth = torch.empty((h, w), dtype=torch.float32, device="cuda")
     pts = torch.empty((h * w if gen_point_cloud else 1, 4), dtype=torch.float32, device="cuda")
     n = torch.zeros(1, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = _side_stream(torch)
     engine.depth_points(d.data_ptr(), w, w, h, q_terms(Q), depth_min, depth_max,
                         c.data_ptr() if c is not None else None, w * ch, ch, depth.data_ptr(), w,
                         pts.data_ptr() if gen_point_cloud else None, h * w if gen_point_cloud else 0,
-                        n.data_ptr(), stream)
-    torch.cuda.current_stream().synchronize()
+                        n.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
     k = int(n.item())
     p = pts[:k].cpu().numpy() if gen_point_cloud else np.zeros((0, 4), np.float32)
     return depth.cpu().numpy(), p[:, :3].copy(), p[:, 3].copy().view(np.uint32)

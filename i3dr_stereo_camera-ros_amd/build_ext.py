@@ -17,7 +17,7 @@ LIB = os.path.join(LIBDIR, "libsgm_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["census_sgm.hip", "ocv_sgm.hip", "post.hip", "depth.hip", "sgm_api.cpp"]
+SOURCES = ["census_sgm.hip", "ocv_sgm.hip", "post.hip", "depth.hip", "rectify.hip", "sgm_api.cpp"]
 HEADERS = ["sgm_device.h"]
 
 

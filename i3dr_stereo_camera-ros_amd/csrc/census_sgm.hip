@@ -471,9 +471,15 @@ __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 
     }
 }
 
-// LDS bytes of one WTA row (per-row S slices + RowLds)
+// LDS bytes of one WTA row: the per-row S slices share their space with RowLds::key (the
+// slices are dead before row_finish), then the rest of RowLds
 template <int DPL>
-__host__ __device__ constexpr size_t wta_lds_bytes(int W) { return (size_t)kWG * DPL * 2 + RowLds::bytes(W); }
+__host__ __device__ constexpr size_t wta_key_bytes(int W)
+{
+    return (size_t)kWG * DPL * 2 > (size_t)4 * W ? (size_t)kWG * DPL * 2 : (size_t)4 * W;
+}
+template <int DPL>
+__host__ __device__ constexpr size_t wta_lds_bytes(int W) { return wta_key_bytes<DPL>(W) + RowLds::rest_bytes(W); }
 
 // One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
 template <int DPL, bool EXACT>
@@ -482,10 +488,10 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
 {
     constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
     uint32_t* sl = lds;                           // 4 waves x 4 rows x 16*DPL u16 S values
-    RowLds R(lds + kWG * DPL / 2, g.W);
+    RowLds R(lds, (char*)lds + wta_key_bytes<DPL>(g.W), g.W);   // R.key aliases sl
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane >> 4, p = lane & 15;
-    R.init(g, tid, kWG);
+    R.init(g, tid, kWG, false);
     const bool lane_act = EXACT || p * DPL < g.D;
     // wave-uniform 64-bit volume row base (a C5 volume is 5.5 GB) + 32-bit lane offsets:
     // SGPR-base + VGPR-offset addressing
@@ -565,6 +571,7 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
 #pragma unroll
             for (int j = 0; j < NWD; j++) cur[vv][j] = nxt[vv][j];
     }
+    R.init_key(g, tid, kWG);                      // the S slices are dead: key takes their space
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 

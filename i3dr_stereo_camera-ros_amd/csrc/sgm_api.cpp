@@ -25,6 +25,12 @@ hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint6
 int census_path_items(const Geom&, int, int, int, uint32_t*, int);
 hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t);
 hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
+hipError_t launch_rectify_map(const double*, const double*, const double*, int, int, float*, float*, size_t,
+                              hipStream_t);
+hipError_t launch_remap_cubic(const uint8_t*, size_t, int, int, const float*, const float*, size_t, int, int,
+                              const int16_t*, uint8_t*, size_t, hipStream_t);
+void cubic_table(int16_t*);
+bool rectify_inverse(const double*, const double*, double*);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t,
                                hipStream_t);
@@ -123,6 +129,7 @@ struct sgm_handle {
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
     std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
+    int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
 };
 
 namespace {
@@ -549,6 +556,7 @@ void sgm_destroy(sgm_handle* h)
         if (h->pin) (void)hipHostFree(h->pin);
         if (h->items_pin) (void)hipHostFree(h->items_pin);
         if (h->aux) (void)hipFree(h->aux);
+        if (h->cubic_tab) (void)hipFree(h->cubic_tab);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
@@ -637,6 +645,54 @@ int sgm_disparity_to_msg(sgm_handle* h, const int16_t* d_disp, size_t disp_strid
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     HIP_TRY(sgm::launch_disp_to_msg(d_disp, disp_stride, W, H, min_disparity, max_disparity, d_out, out_stride, st),
             "disp_to_msg");
+    return SGM_OK;
+}
+
+int sgm_rectify_map(sgm_handle* h, const double K[9], const double* dist, int n_dist, const double R[9],
+                    const double P[12], int W, int H, float* d_map_x, float* d_map_y, size_t map_stride, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!K || !P || !d_map_x || !d_map_y || W <= 0 || H <= 0 || map_stride < (size_t)W || (n_dist > 0 && !dist))
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    if (n_dist != 0 && n_dist != 4 && n_dist != 5 && n_dist != 8 && n_dist != 12)
+        return fail(h, SGM_ERR_UNSUPPORTED, "distortion vector must have 0, 4, 5, 8 or 12 elements");
+    double d12[12] = {};
+    for (int i = 0; i < n_dist; i++) d12[i] = dist[i];
+    double ir[9];
+    if (!sgm::rectify_inverse(P, R, ir)) return fail(h, SGM_ERR_ARG, "singular P[:, :3] * R");
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    HIP_TRY(sgm::launch_rectify_map(K, d12, ir, W, H, d_map_x, d_map_y, map_stride, st), "rectify_map");
+    return SGM_OK;
+}
+
+void sgm_cubic_table(int16_t* tab) { if (tab) sgm::cubic_table(tab); }
+
+int sgm_remap_cubic(sgm_handle* h, const uint8_t* d_src, size_t src_stride, int src_w, int src_h, const float* d_map_x,
+                    const float* d_map_y, size_t map_stride, int W, int H, uint8_t* d_dst, size_t dst_stride,
+                    void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!d_src || !d_map_x || !d_map_y || !d_dst || W <= 0 || H <= 0 || src_w <= 0 || src_h <= 0 ||
+        src_stride < (size_t)src_w || map_stride < (size_t)W || dst_stride < (size_t)W)
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (!h->cubic_tab) {      // built on the host once per handle, uploaded synchronously
+        std::vector<int16_t> tab(32 * 32 * 16);
+        sgm::cubic_table(tab.data());
+        int16_t* d = nullptr;
+        HIP_TRY(hipMalloc(&d, tab.size() * 2), "hipMalloc cubic table");
+        hipError_t e = hipMemcpy(d, tab.data(), tab.size() * 2, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(d); return hip_fail(h, e, "upload cubic table"); }
+        h->cubic_tab = d;
+    }
+    HIP_TRY(sgm::launch_remap_cubic(d_src, src_stride, src_w, src_h, d_map_x, d_map_y, map_stride, W, H,
+                                    h->cubic_tab, d_dst, dst_stride, st), "remap_cubic");
     return SGM_OK;
 }
 

@@ -246,17 +246,26 @@ struct CensusFrames {
 struct RowLds {
     uint32_t* key; int16_t* drow; int16_t* bst; uint16_t* mins;
     static size_t bytes(int W) { return (size_t)4 * W + (size_t)6 * (W + 64) + 16; }
-    __device__ RowLds(void* base, int W) {
-        key = (uint32_t*)base;
-        drow = (int16_t*)(key + W);
+    __device__ RowLds(void* base, int W) : RowLds(base, (uint32_t*)base + W, W) {}
+    // key at key_base, the rest at rest (key may alias scratch the caller uses before
+    // row_finish: then init(.., false) and init_key() afterwards)
+    __device__ RowLds(void* key_base, void* rest, int W) {
+        key = (uint32_t*)key_base;
+        drow = (int16_t*)rest;
         bst = drow + W + 64;
         mins = (uint16_t*)(bst + W + 64);
     }
-    __device__ void init(const Geom& g, int tid, int nthr) {
+    static size_t rest_bytes(int W) { return (size_t)6 * (W + 64) + 16; }
+    __device__ void init(const Geom& g, int tid, int nthr, bool with_key = true) {
         for (int x = tid; x < g.W; x += nthr) {
-            key[x] = 0xFFFFFFFFu; drow[x] = (int16_t)g.invalid; bst[x] = -1; mins[x] = 32767;
+            if (with_key) key[x] = 0xFFFFFFFFu;
+            drow[x] = (int16_t)g.invalid; bst[x] = -1; mins[x] = 32767;
         }
         __syncthreads();
+    }
+    __device__ void init_key(const Geom& g, int tid, int nthr) {
+        __syncthreads();
+        for (int x = tid; x < g.W; x += nthr) key[x] = 0xFFFFFFFFu;
     }
 };
 

@@ -182,6 +182,29 @@ int  sgm_depth_points(sgm_handle* h, const float* d_disp, size_t disp_stride, in
                       double depth_min, double depth_max, float* d_depth, size_t depth_stride,
                       sgm_point_xyzrgb* d_points, int max_points, int* d_num_points, void* stream);
 
+/* ---- rectification: the node's rectify(), generate_disparity.cpp:370-386
+ * and rectify.cpp:111-127 — cv::initUndistortRectifyMap(K, D, R, P, size, CV_32FC1) then
+ * cv::remap(INTER_CUBIC, BORDER_CONSTANT 0) — with the map computed once per calibration. */
+
+/* Float rectification maps (map_x, map_y: W x H, row stride map_stride floats) on the device
+ * from the CameraInfo matrices (row-major doubles): K 3x3, D (n_dist = 0, 4, 5, 8 or 12:
+ * k1 k2 p1 p2 [k3 [k4 k5 k6 [s1 s2 s3 s4]]]; the node passes 5), R 3x3 (NULL = identity),
+ * P 3x4 (its left 3x3 is the new camera matrix). Asynchronous on `stream`.
+ * SGM_ERR_UNSUPPORTED for other n_dist (the tilted-sensor model); SGM_ERR_ARG if P*R is
+ * singular.                                                                                */
+int  sgm_rectify_map(sgm_handle* h, const double K[9], const double* D, int n_dist, const double R[9],
+                     const double P[12], int width, int height, float* d_map_x, float* d_map_y,
+                     size_t map_stride, void* stream);
+/* One remapped u8 image: dst(x, y) = bicubic(src at (map_x, map_y)), OpenCV's fixed-point
+ * INTER_CUBIC (1/32 px positions, 15-bit weights), source pixels outside src_w x src_h read
+ * 0. dst is width x height like the maps. Asynchronous on `stream`.                        */
+int  sgm_remap_cubic(sgm_handle* h, const uint8_t* d_src, size_t src_stride, int src_w, int src_h,
+                     const float* d_map_x, const float* d_map_y, size_t map_stride, int width, int height,
+                     uint8_t* d_dst, size_t dst_stride, void* stream);
+/* The 32 x 32 x 16 int16 INTER_CUBIC weight table (entry fy*32 + fx, tap row*4 + col) the
+ * remap uses. Host-only.                                                                   */
+void sgm_cubic_table(int16_t tab[16384]);
+
 /* ---- stage entry points (parity tests compare each stage with the CPU oracle) ----------- */
 /* 9x7 census codes of one image (host buffers; out: W x H uint64, row-major).             */
 int  sgm_debug_census(sgm_handle* h, const uint8_t* img, int width, int height,

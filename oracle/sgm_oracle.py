@@ -257,3 +257,177 @@ def depth_points(disp, Q, depth_min, depth_max, color=None):
             b, g, r = cc[:, 0], cc[:, 1], cc[:, 2]
     rgba = (np.uint32(0xFF000000) | (r << 16) | (g << 8) | b).astype(np.uint32)
     return depth, pts, rgba
+
+
+# ---------------------------------------------------------------------------------------
+# Rectification: the node's rectify() — cv::initUndistortRectifyMap
+# (CV_32FC1 maps) + cv::remap(INTER_CUBIC, BORDER_CONSTANT 0) — generate_disparity.cpp:370-386,
+# rectify.cpp:111-127. OpenCV is absent from the image: this restates its published scalar
+# algorithm (imgproc undistort.cpp / imgwarp.cpp), **parity unpinned** (no fixture holds a
+# rectified image). float32 / float64 numpy arithmetic, one IEEE rounding per operation.
+# ---------------------------------------------------------------------------------------
+INTER_BITS = 5
+INTER_TAB_SIZE = 1 << INTER_BITS          # 32 sub-pixel positions per axis
+INTER_REMAP_COEF_BITS = 15
+INTER_REMAP_COEF_SCALE = 1 << INTER_REMAP_COEF_BITS
+
+
+def _cubic_coeffs(x):
+    """imgwarp.cpp interpolateCubic (float, A = -0.75)."""
+    f = np.float32
+    A, x = f(-0.75), f(x)
+    one = f(1)
+    c0 = ((A * (x + one) - f(5) * A) * (x + one) + f(8) * A) * (x + one) - f(4) * A
+    c1 = ((A + f(2)) * x - (A + f(3))) * x * x + one
+    c2 = ((A + f(2)) * (one - x) - (A + f(3))) * (one - x) * (one - x) + one
+    c3 = one - c0 - c1 - c2
+    return [c0, c1, c2, c3]
+
+
+def cubic_table():
+    """initInterTab2D(INTER_CUBIC, fixpt=true): int16 [32*32][16] weights, entry (fy*32 + fx),
+    tap k1*4 + k2 = row sy-1+k1, column sx-1+k2. The float products are rounded to 1/32768
+    (cvRound: half to even); an entry whose sum misses 32768 gets the difference on the
+    largest (sum < 32768) / smallest (sum > 32768) tap of rows/columns 2..3."""
+    scale = np.float32(1.0) / np.float32(INTER_TAB_SIZE)
+    t1 = [_cubic_coeffs(np.float32(i) * scale) for i in range(INTER_TAB_SIZE)]
+    tab = np.zeros((INTER_TAB_SIZE * INTER_TAB_SIZE, 16), np.int16)
+    for i in range(INTER_TAB_SIZE):
+        for j in range(INTER_TAB_SIZE):
+            it = [0] * 16
+            for k1 in range(4):
+                vy = t1[i][k1]
+                for k2 in range(4):
+                    v = np.float32(vy * t1[j][k2])
+                    r = int(np.rint(np.float32(v * np.float32(INTER_REMAP_COEF_SCALE))))
+                    it[k1 * 4 + k2] = max(-32768, min(32767, r))
+            isum = sum(it)
+            if isum != INTER_REMAP_COEF_SCALE:
+                diff = isum - INTER_REMAP_COEF_SCALE
+                k0 = 2
+                Mk1 = Mk2 = mk1 = mk2 = k0
+                for k1 in range(k0, k0 + 2):
+                    for k2 in range(k0, k0 + 2):
+                        if it[k1 * 4 + k2] < it[mk1 * 4 + mk2]:
+                            mk1, mk2 = k1, k2
+                        elif it[k1 * 4 + k2] > it[Mk1 * 4 + Mk2]:
+                            Mk1, Mk2 = k1, k2
+                if diff < 0:
+                    it[Mk1 * 4 + Mk2] -= diff
+                else:
+                    it[mk1 * 4 + mk2] -= diff
+            tab[i * INTER_TAB_SIZE + j] = it
+    return tab
+
+
+def rectify_inverse(K, P, R=None):
+    """iR = (P[:, :3] * R)^-1 of initUndistortRectifyMap: the 3x3 product summed k = 0..2 in
+    order, the inverse by cv::invert's 3x3 closed form (DECOMP_LU: adjugate * (1 / det3))."""
+    Ar = np.asarray(P, np.float64).reshape(3, -1)[:, :3]
+    R = np.eye(3) if R is None else np.asarray(R, np.float64).reshape(3, 3)
+    M = np.zeros((3, 3))
+    for i in range(3):
+        for j in range(3):
+            s = 0.0
+            for k in range(3):
+                s += Ar[i, k] * R[k, j]
+            M[i, j] = s
+    m = M
+    det = (m[0, 0] * (m[1, 1] * m[2, 2] - m[1, 2] * m[2, 1]) -
+           m[0, 1] * (m[1, 0] * m[2, 2] - m[1, 2] * m[2, 0]) +
+           m[0, 2] * (m[1, 0] * m[2, 1] - m[1, 1] * m[2, 0]))
+    if det == 0.0:
+        raise ValueError("singular P[:, :3] * R")
+    d = 1.0 / det
+    t = [(m[1, 1] * m[2, 2] - m[1, 2] * m[2, 1]) * d,
+         (m[0, 2] * m[2, 1] - m[0, 1] * m[2, 2]) * d,
+         (m[0, 1] * m[1, 2] - m[0, 2] * m[1, 1]) * d,
+         (m[1, 2] * m[2, 0] - m[1, 0] * m[2, 2]) * d,
+         (m[0, 0] * m[2, 2] - m[0, 2] * m[2, 0]) * d,
+         (m[0, 2] * m[1, 0] - m[0, 0] * m[1, 2]) * d,
+         (m[1, 0] * m[2, 1] - m[1, 1] * m[2, 0]) * d,
+         (m[0, 1] * m[2, 0] - m[0, 0] * m[2, 1]) * d,
+         (m[0, 0] * m[1, 1] - m[0, 1] * m[1, 0]) * d]
+    return np.array(t, np.float64)
+
+
+def dist_coeffs(D):
+    """OpenCV's 4/5/8/12-element distortion vector -> k1 k2 p1 p2 k3 k4 k5 k6 s1 s2 s3 s4."""
+    D = [] if D is None else [float(v) for v in np.asarray(D, np.float64).ravel()]
+    if len(D) not in (0, 4, 5, 8, 12):
+        raise ValueError("distortion vector must have 0, 4, 5, 8 or 12 elements")
+    return np.array(D + [0.0] * (12 - len(D)), np.float64)
+
+
+def rectify_map(K, D, R, P, width, height):
+    """initUndistortRectifyMap(K, D, R, P, (W, H), CV_32FC1) — the scalar loop: per row i,
+    _x = i*ir1 + ir2 (etc.), advanced by += ir0 per column; per pixel the rational + tangential
+    + thin-prism model, identity tilt, u = fx*invProj*xt + u0, stored as float.
+    Returns (map_x, map_y) float32 HxW."""
+    K = np.asarray(K, np.float64).reshape(3, 3)
+    ir = rectify_inverse(K, P, R)
+    k1, k2, p1, p2, k3, k4, k5, k6, s1, s2, s3, s4 = dist_coeffs(D)
+    u0, v0, fx, fy = K[0, 2], K[1, 2], K[0, 0], K[1, 1]
+    i = np.arange(height, dtype=np.float64)[:, None]
+
+    def run(c_i, c_0, c_j):      # row start i*c_i + c_0, then sequential += c_j
+        a = np.empty((height, width), np.float64)
+        a[:, :1] = i * c_i + c_0
+        a[:, 1:] = c_j
+        return np.cumsum(a, axis=1)    # np.add.accumulate: strictly left-to-right
+    _x, _y, _w = run(ir[1], ir[2], ir[0]), run(ir[4], ir[5], ir[3]), run(ir[7], ir[8], ir[6])
+    with np.errstate(all="ignore"):
+        w = 1.0 / _w
+        x = _x * w
+        y = _y * w
+        x2 = x * x
+        y2 = y * y
+        r2 = x2 + y2
+        _2xy = 2 * x * y
+        kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2)
+        xd = x * kr + p1 * _2xy + p2 * (r2 + 2 * x2) + s1 * r2 + s2 * r2 * r2
+        yd = y * kr + p1 * (r2 + 2 * y2) + p2 * _2xy + s3 * r2 + s4 * r2 * r2
+        # matTilt (identity) * (xd, yd, 1): Matx product, s = 0; s += a(i,k) * b(k)
+        t0 = ((0.0 + 1.0 * xd) + 0.0 * yd) + 0.0 * 1.0
+        t1 = ((0.0 + 0.0 * xd) + 1.0 * yd) + 0.0 * 1.0
+        t2 = ((0.0 + 0.0 * xd) + 0.0 * yd) + 1.0 * 1.0
+        inv = np.where(t2 != 0, 1.0 / np.where(t2 != 0, t2, 1.0), 1.0)
+        u = fx * inv * t0 + u0
+        v = fy * inv * t1 + v0
+    return u.astype(np.float32), v.astype(np.float32)
+
+
+def _round_sat_int(v):
+    """saturate_cast<int>(float) = cvRound: half to even; out of range / NaN -> INT_MIN
+    (cvtss2si's integer indefinite)."""
+    v = np.asarray(v, np.float32)
+    ok = (v > np.float32(-2147483648.0)) & (v < np.float32(2147483648.0))
+    r = np.rint(np.where(ok, v, 0)).astype(np.int64)
+    return np.where(ok, r, -2147483648).astype(np.int64)
+
+
+def remap_cubic(src, map_x, map_y, tab=None):
+    """cv::remap(src, dst, map_x, map_y, INTER_CUBIC, BORDER_CONSTANT, 0) for u8 mono:
+    X = cvRound(map_x * 32) -> integer part saturate_cast<short>(X >> 5), fraction X & 31 (same
+    for Y); dst = saturate_u8((sum over in-image taps of src * w + 2^14) >> 15), taps outside
+    the image read the border value 0."""
+    src = np.asarray(src, np.uint8)
+    sh, sw = src.shape
+    tab = cubic_table() if tab is None else tab
+    X = _round_sat_int(np.asarray(map_x, np.float32) * np.float32(INTER_TAB_SIZE))
+    Y = _round_sat_int(np.asarray(map_y, np.float32) * np.float32(INTER_TAB_SIZE))
+    fxy = (Y & (INTER_TAB_SIZE - 1)) * INTER_TAB_SIZE + (X & (INTER_TAB_SIZE - 1))
+    sx = np.clip(X >> INTER_BITS, -32768, 32767) - 1
+    sy = np.clip(Y >> INTER_BITS, -32768, 32767) - 1
+    w = tab[fxy].astype(np.int64)                   # H x W x 16
+    acc = np.zeros(X.shape, np.int64)
+    s64 = src.astype(np.int64)
+    for k1 in range(4):
+        yy = sy + k1
+        oky = (yy >= 0) & (yy < sh)
+        for k2 in range(4):
+            xx = sx + k2
+            ok = oky & (xx >= 0) & (xx < sw)
+            px = np.where(ok, s64[np.clip(yy, 0, sh - 1), np.clip(xx, 0, sw - 1)], 0)
+            acc += px * w[..., k1 * 4 + k2]
+    return np.clip((acc + (1 << (INTER_REMAP_COEF_BITS - 1))) >> INTER_REMAP_COEF_BITS, 0, 255).astype(np.uint8)

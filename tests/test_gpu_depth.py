@@ -9,6 +9,18 @@ from test_depth_oracle import _q, _sample_disp
 pytestmark = pytest.mark.gpu
 
 
+def _stream(torch):
+    """A side stream ordered after torch's queued work (the library's NULL stream argument
+    means the handle's own stream)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    _stream.keep.append(st)
+    return st.cuda_stream
+
+
+_stream.keep = []
+
+
 def _dev(torch, a):
     return torch.as_tensor(np.ascontiguousarray(a)).cuda()
 
@@ -23,7 +35,7 @@ def test_disparity_to_msg(engine, oracle, shape):
     out = torch.full((h, w + 5), -1.0, dtype=torch.float32, device="cuda")
     for lo, hi in [(0.0, float("inf")), (2.0, 150.0)]:
         engine.disparity_to_msg(src.data_ptr(), w, w, h, lo, hi, out.data_ptr(), w + 5,
-                                torch.cuda.current_stream().cuda_stream)
+                                _stream(torch))
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert np.array_equal(got[:, :w].view(np.uint32), oracle.disparity_to_msg(d16, lo, hi).view(np.uint32))
@@ -59,7 +71,7 @@ def test_depth_points_truncation_and_count(engine, oracle, pkg):
     cap = len(rp) // 3
     pts = torch.full((cap + 8, 4), -7.0, dtype=torch.float32, device="cuda")
     n = torch.zeros(1, dtype=torch.int32, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
+    s = _stream(torch)
     engine.depth_points(dd.data_ptr(), w, w, h, pkg.q_terms(Q), 0.0, 100.0, d_points=pts.data_ptr(), max_points=cap,
                         d_num_points=n.data_ptr(), stream=s)
     torch.cuda.synchronize()
@@ -88,7 +100,7 @@ def test_match_to_cloud_chain(engine, oracle, pkg, synth):
     lo, hi = np.float32(T * f / zmax), np.float32(T * f / zmin)
     src = _dev(torch, disp16)
     msg = torch.empty((h, w), dtype=torch.float32, device="cuda")
-    engine.disparity_to_msg(src.data_ptr(), w, w, h, lo, hi, msg.data_ptr(), w, torch.cuda.current_stream().cuda_stream)
+    engine.disparity_to_msg(src.data_ptr(), w, w, h, lo, hi, msg.data_ptr(), w, _stream(torch))
     torch.cuda.synchronize()
     m = msg.cpu().numpy()
     assert np.array_equal(m.view(np.uint32), oracle.disparity_to_msg(disp16, lo, hi).view(np.uint32))
