@@ -42,7 +42,7 @@ EXPORTS = [
     "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
-    "sgm_remap_cubic", "sgm_cubic_table", "sgm_debug_census",
+    "sgm_remap_cubic", "sgm_cubic_table", "sgm_set_rectification", "sgm_match_device_batch_rect", "sgm_debug_census",
     "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
 ]
 
@@ -122,6 +122,8 @@ def load_library(path=None):
                                   P(ctypes.c_double), ci, ci, vp, vp, sz, vp]
     L.sgm_remap_cubic.argtypes = [vp, vp, sz, ci, ci, vp, vp, sz, ci, ci, vp, sz, vp]
     L.sgm_cubic_table.argtypes = [vp]
+    L.sgm_set_rectification.argtypes = [vp, vp, vp, vp, vp, sz, ci, ci]
+    L.sgm_match_device_batch_rect.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), P(vp), sz, P(vp), sz, vp]
     L.sgm_cubic_table.restype = None
     L.sgm_debug_census.argtypes = [vp, vp, ci, ci, sz, vp]
     L.sgm_debug_census_path.argtypes = [vp, vp, vp, ci, ci, sz, ci, vp]
@@ -228,6 +230,26 @@ class Engine:
         self._check(self.lib.sgm_match_device_batch(self.h, arr(*d_lefts), arr(*d_rights), n, width, height, stride,
                                                     arr(*d_outs), out_stride,
                                                     ctypes.c_void_p(stream) if stream else None))
+
+    def set_rectification(self, maps_left=None, maps_right=None, map_stride=0, src_width=0, src_height=0):
+        """Raw inputs from now on: device matches rectify inside the census through the
+        (map_x, map_y) device pointers of each camera (None, None: off)."""
+        vp = ctypes.c_void_p
+        ml = maps_left or (None, None)
+        mr = maps_right or (None, None)
+        self._check(self.lib.sgm_set_rectification(self.h, vp(ml[0]), vp(ml[1]), vp(mr[0]), vp(mr[1]), map_stride,
+                                                   src_width, src_height))
+
+    def match_device_batch_rect(self, d_lefts, d_rights, width, height, raw_stride, d_rect_lefts, d_rect_rights,
+                                rect_stride, d_outs, out_stride, stream=None):
+        """match_device_batch on raw frames that also returns the rectified images."""
+        n = len(d_lefts)
+        arr = ctypes.c_void_p * max(n, 1)
+        rl = arr(*d_rect_lefts) if d_rect_lefts is not None else None
+        rr = arr(*d_rect_rights) if d_rect_rights is not None else None
+        self._check(self.lib.sgm_match_device_batch_rect(self.h, arr(*d_lefts), arr(*d_rights), n, width, height,
+                                                         raw_stride, rl, rr, rect_stride, arr(*d_outs), out_stride,
+                                                         ctypes.c_void_p(stream) if stream else None))
 
     def synchronize(self):
         self._check(self.lib.sgm_synchronize(self.h))

@@ -613,10 +613,26 @@ __device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int 
     uint64_t* out = (img & 1) ? pick4(cf.cR, f) : pick4(cf.cL, f);
     const int x0 = (r - by * bx) * 64, y0 = by * kCensusRows;
     constexpr int TH = kCensusRows + 6;
-    for (int i = threadIdx.x; i < TH * 72; i += kWG) {
-        const int ty = i / 72, tx = i - ty * 72;
-        const int yy = min(max(y0 + ty - 3, 0), H - 1), xx = min(max(x0 + tx - 4, 0), W - 1);
-        tile[i] = src[(size_t)yy * cf.stride + xx];
+    if (cf.rect.tab) {      // rectify on the fly: tile = remap(raw) at the clamped positions
+        const float* mx = cf.rect.map[(img & 1) * 2];
+        const float* my = cf.rect.map[(img & 1) * 2 + 1];
+        uint8_t* rect = (img & 1) ? pick4(cf.rectR, f) : pick4(cf.rectL, f);
+        for (int i = threadIdx.x; i < TH * 72; i += kWG) {
+            const int ty = i / 72, tx = i - ty * 72;
+            const int yy = min(max(y0 + ty - 3, 0), H - 1), xx = min(max(x0 + tx - 4, 0), W - 1);
+            const size_t m = (size_t)yy * cf.rect.map_stride + xx;
+            const uint8_t v = remap_cubic_px(src, cf.stride, cf.rect.src_w, cf.rect.src_h, mx[m], my[m], cf.rect.tab);
+            tile[i] = v;
+            // each rectified pixel is written by the one block whose interior holds it
+            if (rect && ty >= 3 && ty < 3 + kCensusRows && tx >= 4 && tx < 68 && y0 + ty - 3 < H && x0 + tx - 4 < W)
+                rect[(size_t)yy * cf.rect_stride + xx] = v;
+        }
+    } else {
+        for (int i = threadIdx.x; i < TH * 72; i += kWG) {
+            const int ty = i / 72, tx = i - ty * 72;
+            const int yy = min(max(y0 + ty - 3, 0), H - 1), xx = min(max(x0 + tx - 4, 0), W - 1);
+            tile[i] = src[(size_t)yy * cf.stride + xx];
+        }
     }
     __syncthreads();
     const int tx = threadIdx.x & 63, x = x0 + tx;
@@ -639,6 +655,13 @@ __device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int 
         }
         out[(size_t)y * W + x] = code;
     }
+}
+
+// census (optionally rectifying) of all frames of cf on its own: one block per 64 x 32 tile
+__global__ __launch_bounds__(kWG) void k_census_tiles(CensusFrames cf, int W, int H)
+{
+    __shared__ uint8_t tile[(kCensusRows + 6) * 72];
+    census_block(cf, W, H, blockIdx.x, tile);
 }
 
 // blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf
@@ -842,6 +865,13 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
         hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
                            pl, items, n_items, out_stride, period, tr);
     trace_dump(tr, (int)grid.x, st);
+}
+
+hipError_t launch_census_tiles(const CensusFrames& cf, int W, int H, hipStream_t st)
+{
+    const int n = ((W + 63) / 64) * ((H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
+    if (n > 0) hipLaunchKernelGGL(k_census_tiles, dim3(n), dim3(kWG), 0, st, cf, W, H);
+    return hipGetLastError();
 }
 
 // One launch: path sweeps of the frames in pf (items), WTA of the frames in wf (the previous

@@ -67,14 +67,6 @@ __global__ __launch_bounds__(64) void k_rectify_map(RectMap m, int W, int H, flo
     }
 }
 
-// saturate_cast<int>(float): round half to even, out of range / NaN -> INT_MIN
-__device__ __forceinline__ int round_sat_int(float v)
-{
-    return (v > -2147483648.0f && v < 2147483648.0f) ? (int)__builtin_rintf(v) : (int)0x80000000u;
-}
-
-__device__ __forceinline__ int sat_short(int v) { return min(max(v, -32768), 32767); }
-
 // One output pixel per thread; a 64 x 4 block covers 64 consecutive columns of 4 rows.
 __global__ __launch_bounds__(256) void k_remap_cubic(const uint8_t* __restrict__ src, size_t sstride, int sw, int sh,
                                                      const float* __restrict__ mx, const float* __restrict__ my,
@@ -83,30 +75,8 @@ __global__ __launch_bounds__(256) void k_remap_cubic(const uint8_t* __restrict__
 {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= W || y >= H) return;
-    const int X = round_sat_int(mx[(size_t)y * mstride + x] * (float)kInterTab);
-    const int Y = round_sat_int(my[(size_t)y * mstride + x] * (float)kInterTab);
-    const int sx = sat_short(X >> kInterBits) - 1, sy = sat_short(Y >> kInterBits) - 1;
-    const int16_t* w = tab + (size_t)(((Y & (kInterTab - 1)) * kInterTab + (X & (kInterTab - 1))) * 16);
-    int sum = 0;
-    if ((unsigned)sx < (unsigned)max(sw - 3, 0) && (unsigned)sy < (unsigned)max(sh - 3, 0)) {
-        const uint8_t* s = src + (size_t)sy * sstride + sx;
-#pragma unroll
-        for (int k1 = 0; k1 < 4; k1++, s += sstride)
-#pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) sum += (int)s[k2] * (int)w[k1 * 4 + k2];
-    } else {
-#pragma unroll
-        for (int k1 = 0; k1 < 4; k1++) {
-            const int yy = sy + k1;
-            if (yy < 0 || yy >= sh) continue;
-#pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) {
-                const int xx = sx + k2;
-                if (xx >= 0 && xx < sw) sum += (int)src[(size_t)yy * sstride + xx] * (int)w[k1 * 4 + k2];
-            }
-        }
-    }
-    dst[(size_t)y * dstride + x] = (uint8_t)min(max((sum + (1 << (kCoefBits - 1))) >> kCoefBits, 0), 255);
+    const size_t m = (size_t)y * mstride + x;
+    dst[(size_t)y * dstride + x] = remap_cubic_px(src, sstride, sw, sh, mx[m], my[m], tab);
 }
 
 // ---- host -------------------------------------------------------------------------------

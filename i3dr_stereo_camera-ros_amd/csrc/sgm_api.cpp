@@ -31,6 +31,7 @@ hipError_t launch_remap_cubic(const uint8_t*, size_t, int, int, const float*, co
                               const int16_t*, uint8_t*, size_t, hipStream_t);
 void cubic_table(int16_t*);
 bool rectify_inverse(const double*, const double*, double*);
+hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t,
                                hipStream_t);
@@ -130,6 +131,8 @@ struct sgm_handle {
     int items_cap = 0;
     std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
     int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
+    bool rect_on = false;          // sgm_set_rectification: batch inputs are raw, rectified in the census
+    sgm::RectifyIn rect{};
 };
 
 namespace {
@@ -208,6 +211,21 @@ int ensure_pin(sgm_handle* h, size_t bytes)
     hipError_t e = hipHostMalloc((void**)&h->pin, bytes, hipHostMallocDefault);
     if (e != hipSuccess) { h->pin = nullptr; return fail(h, SGM_ERR_ALLOC, "hipHostMalloc staging"); }
     h->pin_size = bytes;
+    return SGM_OK;
+}
+
+// The INTER_CUBIC weight table on the device, built on the host once per handle.
+int ensure_cubic_table(sgm_handle* h)
+{
+    if (h->cubic_tab) return SGM_OK;
+    std::vector<int16_t> tab(32 * 32 * 16);
+    sgm::cubic_table(tab.data());
+    int16_t* d = nullptr;
+    hipError_t e = hipMalloc(&d, tab.size() * 2);
+    if (e != hipSuccess) return hip_fail(h, e, "hipMalloc cubic table");
+    e = hipMemcpy(d, tab.data(), tab.size() * 2, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(d); return hip_fail(h, e, "upload cubic table"); }
+    h->cubic_tab = d;
     return SGM_OK;
 }
 
@@ -409,8 +427,12 @@ int batch_group(int n)
 // the previous launch. With a median the WTA of a group writes each frame's raw disparity
 // to its own scratch image (post filters read it), so no frame's output is overwritten
 // before its median.
+// With h->rect_on, dLs / dRs are raw images (stride = raw stride) rectified inside the census
+// (the census tiles read remap(raw)), and rectLs / rectRs (may be null) receive the
+// rectified images.
 int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* const* dLs,
-                     const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride)
+                     const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride,
+                     uint8_t* const* rectLs = nullptr, uint8_t* const* rectRs = nullptr, size_t rect_stride = 0)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
@@ -451,19 +473,28 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         sgm::CensusFrames cf{};
         cf.n = frames_of(k);
         cf.stride = stride;
+        cf.rect_stride = rect_stride;
+        if (h->rect_on) cf.rect = h->rect;
         for (int f = 0; f < cf.n; f++) {
             const int set = (k & 1) * G + f;
             cf.L[f] = dLs[k * G + f];
             cf.R[f] = dRs[k * G + f];
             cf.cL[f] = (uint64_t*)(ws + l.cL[set]);
             cf.cR[f] = (uint64_t*)(ws + l.cR[set]);
+            cf.rectL[f] = rectLs ? rectLs[k * G + f] : nullptr;
+            cf.rectR[f] = rectRs ? rectRs[k * G + f] : nullptr;
         }
         return cf;
     };
-    for (int f = 0; f < frames_of(0); f++) {
-        rec.begin("census", 2 * WH + 16 * WH);
-        HIP_TRY(sgm::launch_census(dLs[f], dRs[f], stride, g.W, g.H, (uint64_t*)(ws + l.cL[f]),
-                                   (uint64_t*)(ws + l.cR[f]), st), "census");
+    if (h->rect_on) {           // remap + census of the first group, one launch
+        rec.begin("rectify+census", (2 * WH + 16 * WH + 16 * WH) * frames_of(0));
+        HIP_TRY(sgm::launch_census_tiles(census_frames(0), g.W, g.H, st), "rectify+census");
+    } else {
+        for (int f = 0; f < frames_of(0); f++) {
+            rec.begin("census", 2 * WH + 16 * WH);
+            HIP_TRY(sgm::launch_census(dLs[f], dRs[f], stride, g.W, g.H, (uint64_t*)(ws + l.cL[f]),
+                                       (uint64_t*)(ws + l.cR[f]), st), "census");
+        }
     }
     for (int k = 0; k <= ng; k++) {
         if (k == ng) {
@@ -592,6 +623,12 @@ int sgm_match_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W,
                      size_t out_stride, void* stream)
 {
     if (!h) return SGM_ERR_ARG;
+    if (h->rect_on) {          // raw inputs: the census-fused rectification path
+        const uint8_t* l1[1] = {dL};
+        const uint8_t* r1[1] = {dR};
+        int16_t* o1[1] = {dOut};
+        return sgm_match_device_batch_rect(h, l1, r1, 1, W, H, stride, nullptr, nullptr, 0, o1, out_stride, stream);
+    }
     std::lock_guard<std::mutex> lk(h->mu);
     if (!dL || !dR || !dOut || stride < (size_t)W || out_stride < (size_t)W) return fail(h, SGM_ERR_ARG, "bad buffers");
     Geom g;
@@ -605,32 +642,62 @@ int sgm_match_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W,
     return rc;
 }
 
-int sgm_match_device_batch(sgm_handle* h, const uint8_t* const* dLs, const uint8_t* const* dRs, int n, int W, int H,
-                           size_t stride, int16_t* const* outs, size_t out_stride, void* stream)
+int sgm_match_device_batch_rect(sgm_handle* h, const uint8_t* const* dLs, const uint8_t* const* dRs, int n, int W,
+                                int H, size_t stride, uint8_t* const* rectLs, uint8_t* const* rectRs,
+                                size_t rect_stride, int16_t* const* outs, size_t out_stride, void* stream)
 {
     if (!h) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
-    if (n < 0 || (n > 0 && (!dLs || !dRs || !outs)) || stride < (size_t)W || out_stride < (size_t)W)
+    const size_t in_w = h->rect_on ? (size_t)h->rect.src_w : (size_t)W;
+    if (n < 0 || (n > 0 && (!dLs || !dRs || !outs)) || stride < in_w || out_stride < (size_t)W)
         return fail(h, SGM_ERR_ARG, "bad buffers");
+    if ((rectLs || rectRs) && (!h->rect_on || rect_stride < (size_t)W))
+        return fail(h, SGM_ERR_ARG, "rectified outputs need sgm_set_rectification and rect_stride >= width");
     for (int i = 0; i < n; i++)
         if (!dLs[i] || !dRs[i] || !outs[i]) return fail(h, SGM_ERR_ARG, "null frame pointer");
     if (n == 0) return SGM_OK;
+    if (h->rect_on && h->params.mode != SGM_MODE_CENSUS8)
+        return fail(h, SGM_ERR_UNSUPPORTED, "fused rectification runs in the census mode (use sgm_remap_cubic)");
     Geom g;
     Layout l;
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
-    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2 && g.width1 > 0;
+    if (h->rect_on && g.width1 <= 0)
+        return fail(h, SGM_ERR_UNSUPPORTED, "fused rectification needs a non-empty disparity window");
+    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && (n >= 2 || h->rect_on) && g.width1 > 0;
     rc = prepare(h, W, H, false, g, l, pipelined ? batch_group(n) : 0);
     if (rc) return rc;
     hipStream_t own = h->stream;
     if (stream) h->stream = (hipStream_t)stream;
     if (pipelined) {
-        rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride);
+        rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride, rectLs, rectRs, rect_stride);
     } else {
         for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
     }
     h->stream = own;
     return rc;
+}
+
+int sgm_match_device_batch(sgm_handle* h, const uint8_t* const* dLs, const uint8_t* const* dRs, int n, int W, int H,
+                           size_t stride, int16_t* const* outs, size_t out_stride, void* stream)
+{
+    return sgm_match_device_batch_rect(h, dLs, dRs, n, W, H, stride, nullptr, nullptr, 0, outs, out_stride, stream);
+}
+
+int sgm_set_rectification(sgm_handle* h, const float* d_map_xl, const float* d_map_yl, const float* d_map_xr,
+                          const float* d_map_yr, size_t map_stride, int src_w, int src_h)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!d_map_xl && !d_map_yl && !d_map_xr && !d_map_yr) { h->rect_on = false; return SGM_OK; }
+    if (!d_map_xl || !d_map_yl || !d_map_xr || !d_map_yr || src_w <= 0 || src_h <= 0 || map_stride == 0)
+        return fail(h, SGM_ERR_ARG, "rectification needs four maps and the raw image size");
+    int rc = ensure_stream(h);
+    if (rc) return rc;
+    if ((rc = ensure_cubic_table(h))) return rc;
+    h->rect = sgm::RectifyIn{{d_map_xl, d_map_yl, d_map_xr, d_map_yr}, map_stride, src_w, src_h, h->cubic_tab};
+    h->rect_on = true;
+    return SGM_OK;
 }
 
 int sgm_disparity_to_msg(sgm_handle* h, const int16_t* d_disp, size_t disp_stride, int W, int H, float min_disparity,
@@ -682,15 +749,7 @@ int sgm_remap_cubic(sgm_handle* h, const uint8_t* d_src, size_t src_stride, int 
     int rc = ensure_stream(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (!h->cubic_tab) {      // built on the host once per handle, uploaded synchronously
-        std::vector<int16_t> tab(32 * 32 * 16);
-        sgm::cubic_table(tab.data());
-        int16_t* d = nullptr;
-        HIP_TRY(hipMalloc(&d, tab.size() * 2), "hipMalloc cubic table");
-        hipError_t e = hipMemcpy(d, tab.data(), tab.size() * 2, hipMemcpyHostToDevice);
-        if (e != hipSuccess) { (void)hipFree(d); return hip_fail(h, e, "upload cubic table"); }
-        h->cubic_tab = d;
-    }
+    if ((rc = ensure_cubic_table(h))) return rc;
     HIP_TRY(sgm::launch_remap_cubic(d_src, src_stride, src_w, src_h, d_map_x, d_map_y, map_stride, W, H,
                                     h->cubic_tab, d_dst, dst_stride, st), "remap_cubic");
     return SGM_OK;
@@ -757,6 +816,7 @@ int sgm_match(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, s
 {
     if (!h) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
+    if (h->rect_on) return fail(h, SGM_ERR_UNSUPPORTED, "fused rectification applies to device-buffer matches");
     if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W)
         return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
     Geom g;

@@ -233,15 +233,62 @@ struct WtaFrames {
     int16_t* out[kMaxGroup];
     int n;
 };
-// census transforms of the next group, run in the tail of a fused launch
+// Rectification fused into the census: the census tile reads
+// remap(raw, map) instead of a rectified image. map[0..1] = left x/y, map[2..3] = right x/y,
+// each W x H of the rectified geometry; the raw images are src_w x src_h.
+struct RectifyIn {
+    const float* map[4];
+    size_t map_stride;
+    int src_w, src_h;
+    const int16_t* tab;          // INTER_CUBIC weights (rectify.hip cubic_table)
+};
+// census transforms of the next group, run in the tail of a fused launch. With rect.tab
+// set, L/R are raw images (stride = raw stride) and the rectified pixels are also written
+// to rectL/rectR (when not null).
 struct CensusFrames {
     const uint8_t* L[kMaxGroup];
     const uint8_t* R[kMaxGroup];
     uint64_t* cL[kMaxGroup];
     uint64_t* cR[kMaxGroup];
-    size_t stride;
+    uint8_t* rectL[kMaxGroup];
+    uint8_t* rectR[kMaxGroup];
+    size_t stride, rect_stride;
     int n;
+    RectifyIn rect;
 };
+
+// One pixel of cv::remap(src, map_x, map_y, INTER_CUBIC, BORDER_CONSTANT 0) for u8 (rectify.hip)
+__device__ __forceinline__ int remap_round_sat(float v)
+{
+    return (v > -2147483648.0f && v < 2147483648.0f) ? (int)__builtin_rintf(v) : (int)0x80000000u;
+}
+__device__ __forceinline__ uint8_t remap_cubic_px(const uint8_t* __restrict__ src, size_t sstride, int sw, int sh,
+                                                  float fx, float fy, const int16_t* __restrict__ tab)
+{
+    const int X = remap_round_sat(fx * 32.0f), Y = remap_round_sat(fy * 32.0f);
+    const int sx = min(max(X >> 5, -32768), 32767) - 1, sy = min(max(Y >> 5, -32768), 32767) - 1;
+    const int16_t* w = tab + (size_t)(((Y & 31) * 32 + (X & 31)) * 16);
+    int sum = 0;
+    if ((unsigned)sx < (unsigned)max(sw - 3, 0) && (unsigned)sy < (unsigned)max(sh - 3, 0)) {
+        const uint8_t* s = src + (size_t)sy * sstride + sx;
+#pragma unroll
+        for (int k1 = 0; k1 < 4; k1++, s += sstride)
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) sum += (int)s[k2] * (int)w[k1 * 4 + k2];
+    } else {
+#pragma unroll
+        for (int k1 = 0; k1 < 4; k1++) {
+            const int yy = sy + k1;
+            if (yy < 0 || yy >= sh) continue;
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) {
+                const int xx = sx + k2;
+                if (xx >= 0 && xx < sw) sum += (int)src[(size_t)yy * sstride + xx] * (int)w[k1 * 4 + k2];
+            }
+        }
+    }
+    return (uint8_t)min(max((sum + (1 << 14)) >> 15, 0), 255);
+}
 
 struct RowLds {
     uint32_t* key; int16_t* drow; int16_t* bst; uint16_t* mins;

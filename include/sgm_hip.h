@@ -201,6 +201,22 @@ int  sgm_rectify_map(sgm_handle* h, const double K[9], const double* D, int n_di
 int  sgm_remap_cubic(sgm_handle* h, const uint8_t* d_src, size_t src_stride, int src_w, int src_h,
                      const float* d_map_x, const float* d_map_y, size_t map_stride, int width, int height,
                      uint8_t* d_dst, size_t dst_stride, void* stream);
+/* Rectification fused into the census (census mode): after this call the device matches
+ * (sgm_match_device, sgm_match_device_batch, sgm_match_device_batch_rect) take RAW images of
+ * src_width x src_height (their stride argument = the raw stride) and rectify them inside
+ * the census tiles through the maps (W x H = the match geometry, e.g. from sgm_rectify_map;
+ * left x/y, right x/y). The maps must stay valid while set. All four maps NULL switches it
+ * off. sgm_match (host buffers) returns SGM_ERR_UNSUPPORTED while it is on, as do the OCV
+ * modes (rectify those with sgm_remap_cubic).                                               */
+int  sgm_set_rectification(sgm_handle* h, const float* d_map_xl, const float* d_map_yl, const float* d_map_xr,
+                           const float* d_map_yr, size_t map_stride, int src_width, int src_height);
+/* sgm_match_device_batch that also returns the rectified images (d_rect_lefts /
+ * d_rect_rights: arrays of n device pointers, W x H u8 with row stride rect_stride; either
+ * array may be NULL). Needs sgm_set_rectification.                                          */
+int  sgm_match_device_batch_rect(sgm_handle* h, const uint8_t* const* d_raw_lefts, const uint8_t* const* d_raw_rights,
+                                 int n_frames, int width, int height, size_t raw_stride,
+                                 uint8_t* const* d_rect_lefts, uint8_t* const* d_rect_rights, size_t rect_stride,
+                                 int16_t* const* d_disps, size_t out_stride, void* stream);
 /* The 32 x 32 x 16 int16 INTER_CUBIC weight table (entry fy*32 + fx, tap row*4 + col) the
  * remap uses. Host-only.                                                                   */
 void sgm_cubic_table(int16_t tab[16384]);

@@ -87,3 +87,58 @@ def test_rectify_end_to_end(engine, oracle, pkg, synth, w, h):
     assert np.array_equal(got, oracle.remap_cubic(left, rx, ry))
     got2, _ = pkg.rectify(engine, right, K, D, R, P, maps=maps)
     assert np.array_equal(got2, oracle.remap_cubic(right, rx, ry))
+
+
+def _raw_pair(synth, h, w, seed):
+    left, right, _ = synth.stereo_pair(h, w, 0, 48, seed=seed)
+    return left, right
+
+
+@pytest.mark.parametrize("n,raw,rect", [(1, (480, 640), (480, 640)), (3, (500, 700), (432, 608)),
+                                        (5, (240, 320), (240, 320))])
+def test_fused_rectify_census_batch(engine, oracle, pkg, synth, n, raw, rect):
+    """sgm_set_rectification + sgm_match_device_batch_rect: raw frames are rectified inside the
+    census tiles; the disparities equal the oracle's match of the oracle-rectified pair and
+    the rectified images equal the oracle remap (bit-exact)."""
+    torch = pytest.importorskip("torch")
+    from conftest import to_oracle_params
+    (rh, rw), (h, w) = raw, rect
+    KL, DL, RL, PL = calib(seed=11, w=rw, h=rh)
+    KR, DR, RR, PR = calib(seed=12, w=rw, h=rh)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    mxl, myl = _maps(torch, engine, KL, DL, RL, PL, w, h)
+    mxr, myr = _maps(torch, engine, KR, DR, RR, PR, w, h)
+    frames = [_raw_pair(synth, rh, rw, 70 + i) for i in range(n)]
+    dl = [torch.as_tensor(f[0]).cuda() for f in frames]
+    dr = [torch.as_tensor(f[1]).cuda() for f in frames]
+    out = torch.full((n, h, w), 777, dtype=torch.int16, device="cuda")
+    recl = torch.zeros((n, h, w + 8), dtype=torch.uint8, device="cuda")
+    recr = torch.zeros((n, h, w + 8), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    engine.set_rectification((mxl.data_ptr(), myl.data_ptr()), (mxr.data_ptr(), myr.data_ptr()), w, rw, rh)
+    try:
+        engine.match_device_batch_rect([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], w, h, rw,
+                                       [recl[i].data_ptr() for i in range(n)], [recr[i].data_ptr() for i in range(n)],
+                                       w + 8, [out[i].data_ptr() for i in range(n)], w)
+        engine.synchronize()
+        if n == 1:   # the single-frame device entry point takes raw frames too while rectification is on
+            one = torch.full((h, w), 555, dtype=torch.int16, device="cuda")
+            torch.cuda.synchronize()
+            engine.match_device(dl[0].data_ptr(), dr[0].data_ptr(), w, h, rw, one.data_ptr(), w)
+            engine.synchronize()
+        with pytest.raises(pkg.SGMError):          # host-buffer matches are not rectified
+            engine.match(np.zeros((h, w), np.uint8), np.zeros((h, w), np.uint8))
+    finally:
+        engine.set_rectification()
+    rxl, ryl = oracle.rectify_map(KL, DL, RL, PL, w, h)
+    rxr, ryr = oracle.rectify_map(KR, DR, RR, PR, w, h)
+    op = to_oracle_params(oracle, p)
+    got, gl, gr = out.cpu().numpy(), recl.cpu().numpy(), recr.cpu().numpy()
+    for i, (l_raw, r_raw) in enumerate(frames):
+        el, er = oracle.remap_cubic(l_raw, rxl, ryl), oracle.remap_cubic(r_raw, rxr, ryr)
+        assert np.array_equal(gl[i, :, :w], el) and np.array_equal(gr[i, :, :w], er), f"frame {i} rectified"
+        assert (gl[i, :, w:] == 0).all()
+        assert np.array_equal(got[i], oracle.match(op, el, er)), f"frame {i} disparity"
+    if n == 1:
+        assert np.array_equal(one.cpu().numpy(), got[0])
