@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one sgm_match_device call per frame")
+    ap.add_argument("--rectify", action="store_true",
+                    help="raw frames in: rectification (maps of a synthetic calibration) fused into the census")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -154,6 +156,17 @@ def main():
     tstream = torch.cuda.Stream(device)        # the stream every kernel and HIP event runs on
     stream = tstream.cuda_stream
 
+    maps = None
+    if args.rectify:      # maps once per calibration, remap fused with the census
+        f = 0.9 * W
+        K = np.array([[f, 0, W / 2 + 3.3], [0, f * 1.01, H / 2 - 2.1], [0, 0, 1]])
+        Dd = np.array([-0.21, 0.07, 0.0012, -0.0009, -0.011])
+        P = np.array([[0.98 * f, 0, W / 2 - 5.0, 0], [0, 0.98 * f, H / 2 + 1.5, 0], [0, 0, 1, 0]])
+        maps = [torch.empty((H, W), dtype=torch.float32, device=device) for _ in range(2)]
+        eng.rectify_map(K, Dd, None, P, W, H, maps[0].data_ptr(), maps[1].data_ptr(), W)
+        eng.synchronize()
+        eng.set_rectification((maps[0].data_ptr(), maps[1].data_ptr()), (maps[0].data_ptr(), maps[1].data_ptr()),
+                              W, W, H)
     ptr_l = [dl[f % len(dl)].data_ptr() for f in range(args.frames)]
     ptr_r = [dr[f % len(dr)].data_ptr() for f in range(args.frames)]
     ptr_o = [out[f].data_ptr() for f in range(args.frames)]
@@ -220,7 +233,7 @@ def main():
             "config": {"workload": cfg["name"], "width": W, "height": H, "num_disparities": D,
                        "frames_per_rank_per_step": args.frames, "global_batch": args.frames * world,
                        "distinct_frames_per_rank": args.distinct, "parallelism": f"frame-shard x{world}",
-                       "frame_pipeline": not args.no_pipeline},
+                       "frame_pipeline": not args.no_pipeline, "rectify_fused": bool(args.rectify)},
             "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(dom_achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom_achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_launch": dom_bytes,

@@ -614,8 +614,9 @@ __device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int 
     const int x0 = (r - by * bx) * 64, y0 = by * kCensusRows;
     constexpr int TH = kCensusRows + 6;
     if (cf.rect.tab) {      // rectify on the fly: tile = remap(raw) at the clamped positions
-        const float* mx = cf.rect.map[(img & 1) * 2];
-        const float* my = cf.rect.map[(img & 1) * 2 + 1];
+        // (selects, not a dynamic index: that would copy the kernel argument to scratch)
+        const float* mx = (img & 1) ? cf.rect.map[2] : cf.rect.map[0];
+        const float* my = (img & 1) ? cf.rect.map[3] : cf.rect.map[1];
         uint8_t* rect = (img & 1) ? pick4(cf.rectR, f) : pick4(cf.rectL, f);
         for (int i = threadIdx.x; i < TH * 72; i += kWG) {
             const int ty = i / 72, tx = i - ty * 72;

@@ -26,6 +26,7 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   rm -rf gpurun_out/prof
   run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+  python3 tools/prof_compare.py gpurun_out/prof/run_kernel_trace.csv gpurun_out/rocprof.log > gpurun_out/prof_vs_bench.txt
 fi
 exit 0

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 2 --warmup 1 --frames 4 --no-cpu-baseline ${BENCH_ARGS:-}"
+CMD="python3 bench.py --steps 2 --warmup 1 --frames 8 --no-cpu-baseline ${BENCH_ARGS:-}"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \

@@ -13,7 +13,7 @@ import csv
 import glob
 import json
 
-STAGE_OF = {"k_census9x7": "census", "k_census_paths16": "paths8", "k_census_wta16": "wta_lr", "k_census_fused16": "fused",
+STAGE_OF = {"k_census9x7": "census", "k_census_paths16": "paths8", "k_census_wta16": "wta_lr", "k_census_fused16": "fused", "k_census_tiles": "rectify+census",
             "k_ocv_pixcost": "ocv_cost", "k_ocv_paths": "ocv_paths", "k_ocv_wta": "ocv_wta_lr"}
 
 
@@ -24,15 +24,24 @@ def main():
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    grids = collections.defaultdict(set)
     for f in sorted(glob.glob(f"{args.dir}/pass*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            if "k_census_fused16" in k:      # one fused kernel, launches of different content: split by grid
+                k = f"{k}@grid{r['Grid_Size']}"
+                grids[k.split("@")[0]].add(int(r["Grid_Size"]))
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     raw = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
     kernels = {}
     for k, cs in raw.items():
         base = k.split("<")[0].replace("sgm::", "")
         stage = STAGE_OF.get(base)
+        if "@grid" in k:
+            # the steady-state launch (paths of group k + WTA of k-1 + census of k+1) has the
+            # largest grid; the pipeline's ramp launches are reported by grid size
+            g = int(k.split("@grid")[1])
+            stage = "paths8+wta_lr+census" if g == max(grids[k.split("@")[0]]) else f"fused@grid{g}"
         if stage is None or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
         fetch = 2.0 * cs["FETCH_SIZE"] * 1024.0
