@@ -39,7 +39,7 @@ MISSING_Z = 10000.0  # image_geometry::StereoCameraModel::MISSING_Z
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
     "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
-    "sgm_synchronize", "sgm_last_error",
+    "sgm_match_tiled_exact", "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
     "sgm_remap_cubic", "sgm_cubic_table", "sgm_set_rectification", "sgm_match_device_batch_rect", "sgm_debug_census",
@@ -102,6 +102,7 @@ def load_library(path=None):
     L.sgm_match_device_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, vp]
     L.sgm_match_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, P(ci), ci]
     L.sgm_match_tiled.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, ci, P(ci), ci]
+    L.sgm_match_tiled_exact.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, P(ci), ci]
     L.sgm_synchronize.argtypes = [vp]
     L.sgm_last_error.argtypes = [vp]
     L.sgm_last_error.restype = ctypes.c_char_p
@@ -285,6 +286,23 @@ class Engine:
             devs, nd = None, 0
         self._check(self.lib.sgm_match_tiled(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w, n_bands, halo,
                                              devs, nd))
+        return out
+
+    def match_tiled_exact(self, left, right, n_bands, devices=None):
+        """One frame split into row bands over the devices, exact mode: the
+        bands' path sweeps continue across the seams through boundary-row exchanges, so the
+        result equals match() for any band count."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        h, w = left.shape
+        out = np.empty((h, w), np.int16)
+        if devices:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            nd = len(devices)
+        else:
+            devs, nd = None, 0
+        self._check(self.lib.sgm_match_tiled_exact(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w, n_bands,
+                                                   devs, nd))
         return out
 
     # -- profiling -------------------------------------------------------------------------

@@ -71,6 +71,22 @@ __global__ __launch_bounds__(256) void k_census9x7(const uint8_t* __restrict__ L
 // So loops issue a fixed sequence: clamped prefetches, and cells that must not be written
 // (outside the image, d >= D, padding steps) go to a per-volume trash slot.
 // ====================================================================================
+// DPL consecutive u8 costs of one lane (the P16 layout of a volume pixel) as dwords
+template <int DPL>
+__device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 3) / 4])
+{
+    if constexpr (DPL == 2) { wd[0] = *(const uint16_t*)src; }
+    else if constexpr (DPL == 4) { wd[0] = *(const uint32_t*)src; }
+    else if constexpr (DPL == 8) { const uint2 v = *(const uint2*)src; wd[0] = v.x; wd[1] = v.y; }
+    else {
+#pragma unroll
+        for (int q = 0; q < DPL / 16; q++) {
+            const uint4 v = ((const uint4*)src)[q];
+            wd[4 * q] = v.x; wd[4 * q + 1] = v.y; wd[4 * q + 2] = v.z; wd[4 * q + 3] = v.w;
+        }
+    }
+}
+
 // dst_hi: where bytes 16..31 go when DPL == 32 (D not a multiple of 32 leaves the lane that
 // straddles D half valid: its upper half must go to the trash slot, not the next pixel)
 template <int DPL>
@@ -129,6 +145,20 @@ __device__ __forceinline__ uint32_t ham_acc(uint64_t a, uint64_t b, uint32_t acc
     return bcnt_acc((uint32_t)(x >> 32), bcnt_acc((uint32_t)x, acc));
 }
 
+// Relative state of a line from its absolute costs: Lr = Labs - min over the row's D
+template <int DPL>
+__device__ __forceinline__ void p16_relative(const uint32_t (&Labs)[DPL / 2], uint32_t (&Lr)[DPL / 2])
+{
+    constexpr int M = DPL / 2;
+    uint32_t mn = Labs[0];
+#pragma unroll
+    for (int i = 1; i < M; i += 2) mn = (i + 1 < M) ? pk_min3_p(mn, Labs[i], Labs[i + 1]) : pk_min(mn, Labs[i]);
+    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
+    const uint32_t off = mn - kBaseP2;                    // pattern(L) - off = pattern(L - min)
+#pragma unroll
+    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], off);
+}
+
 // One recurrence step of the lane's pairs, costs computed on the fly:
 //   L(d) = C(d) + min(Lr(d), Lr(d-1) + P1, Lr(d+1) + P1, P2),  C(d) = Hamming(cl, crk(d))
 // Lr: relative state (patterns) in/out. Labs: absolute L (patterns) out.
@@ -156,13 +186,7 @@ __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F
         Labs[i] = L;
         Oprev = Onext;
     }
-    uint32_t mn = Labs[0];
-#pragma unroll
-    for (int i = 1; i < M; i += 2) mn = (i + 1 < M) ? pk_min3_p(mn, Labs[i], Labs[i + 1]) : pk_min(mn, Labs[i]);
-    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
-    const uint32_t off = mn - kBaseP2;                    // pattern(L) - off = pattern(L - min)
-#pragma unroll
-    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], off);
+    p16_relative<DPL>(Labs, Lr);
 }
 
 // imask: kInfP in the halves with d >= D (0 elsewhere); start: the relative state of a
@@ -178,9 +202,17 @@ __device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL /
     }
 }
 
+// Row-band exact tile mode (sgm_match_tiled_exact): a band's row sweeps continue the lines
+// of its neighbours. bnd[0] holds the last row of the band above for the downward
+// directions 0, 2, 3 (slots 0, 1, 2), bnd[1] the first row of the band below for the upward
+// directions 1, 4, 5; each slot is width1 * D u8 costs in volume order, bnd_slot bytes
+// apart. Null: the band edge is the image edge (lines start there).
 struct PathLaunch16 {
     int xb_lo[6];        // row sweeps: first base column of the direction
+    const uint8_t* bnd[2];
+    size_t bnd_slot;
 };
+__host__ __device__ constexpr int bnd_slot_of(int dir) { return dir <= 1 ? 0 : (dir == 2 || dir == 4 ? 1 : 2); }
 // Work list entry (one per workgroup): dir << 24 | frame-in-group << 22 | local block.
 __host__ __device__ constexpr uint32_t path_item(int dir, int lb, int f = 0)
 {
@@ -326,10 +358,27 @@ __device__ __forceinline__ void seg_store(uint64_t* buf, const uint64_t (&v)[Row
     }
 }
 
+// Relative state of a line continued from a neighbouring band: the u8 costs Lprev stored
+// for its predecessor pixel (src: the lane's DPL bytes) -> Lprev - min Lprev. Every lane of
+// the row takes part (row-wide min); the caller selects per line.
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void p16_seed(const uint8_t* src, const uint32_t (&imask)[DPL / 2], uint32_t (&Lr)[DPL / 2])
+{
+    uint32_t wd[(DPL + 3) / 4], Labs[DPL / 2];
+    wload<DPL>(src, wd);
+#pragma unroll
+    for (int i = 0; i < DPL / 2; i++) {
+        const uint32_t pr = __builtin_amdgcn_perm(0u, wd[i / 2], (i & 1) ? 0x0c030c02u : 0x0c010c00u);
+        Labs[i] = pr | kBaseP2;                           // bytes -> biased-f16 patterns
+        if (!EXACT) Labs[i] = pk_max(Labs[i], imask[i]);
+    }
+    p16_relative<DPL>(Labs, Lr);
+}
+
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
-                                         int xb, uint64_t* lds)
+                                         int xb, const PathLaunch16& pl, uint64_t* lds)
 {
     using RS = RowSeg<DPL>;
     constexpr int M = DPL / 2;
@@ -350,6 +399,17 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 #pragma unroll
     for (int i = 0; i < M; i++) Lr[i] = start[i];
     bool pv = false;
+    const uint8_t* bnd = pl.bnd[ry > 0 ? 0 : 1];
+    if (bnd && s0 == 0) {                          // exact tile mode: continue the band above / below
+        const int x = xb + j, xp = x - rx;         // the line's pixel at step 0 and its predecessor
+        const bool cont = x >= g.minX1 && x < g.maxX1 && xp >= g.minX1 && xp < g.maxX1;
+        const int xs = min(max(xp, g.minX1), g.maxX1 - 1) - g.minX1;
+        uint32_t Ls[M];
+        p16_seed<DPL, EXACT>(bnd + bnd_slot_of(dir) * pl.bnd_slot + (size_t)xs * g.D + p * DPL, imask, Ls);
+#pragma unroll
+        for (int i = 0; i < M; i++) Lr[i] = cont ? Ls[i] : Lr[i];
+        pv = cont;
+    }
     const bool lane_act = EXACT || p * DPL < g.D;
     const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
     // stores: the step's row base is wave-uniform (64-bit, scalar math); lanes add a 32-bit
@@ -418,7 +478,7 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     uint8_t* trash = V + trash_off;
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-    else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, lds);
+    else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, pl, lds);
 }
 
 // SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
@@ -456,21 +516,6 @@ void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g,
 //  * S[best-1], S[best+1] for the subpixel fit: read back from a per-row LDS slice.
 // Results go to the row's LDS arrays; row_finish() does disp2 (LDS atomics) + LR + store.
 // ====================================================================================
-template <int DPL>
-__device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 3) / 4])
-{
-    if constexpr (DPL == 2) { wd[0] = *(const uint16_t*)src; }
-    else if constexpr (DPL == 4) { wd[0] = *(const uint32_t*)src; }
-    else if constexpr (DPL == 8) { const uint2 v = *(const uint2*)src; wd[0] = v.x; wd[1] = v.y; }
-    else {
-#pragma unroll
-        for (int q = 0; q < DPL / 16; q++) {
-            const uint4 v = ((const uint4*)src)[q];
-            wd[4 * q] = v.x; wd[4 * q + 1] = v.y; wd[4 * q + 2] = v.z; wd[4 * q + 3] = v.w;
-        }
-    }
-}
-
 // LDS bytes of one WTA row: the per-row S slices share their space with RowLds::key (the
 // slices are dead before row_finish), then the rest of RowLds
 template <int DPL>
@@ -717,19 +762,19 @@ PathLaunch16 make_path_launch16(const Geom& g)
 }
 
 // Work list of one paths launch for a group of `group` frames: every 16-line block of
-// every direction (only_dir >= 0: that direction only) of every frame, longest first with
+// every direction in dir_mask (bit d: direction d) of every frame, longest first with
 // the frames of equal-length blocks adjacent, dealt in a snake over rounds of n_slots
 // workgroups (consecutive workgroup ids go to different CUs, so each CU mixes long and
 // short work; with group > 1 there are more blocks than resident slots and the dispatcher
 // hands the short ones to whichever CUs drain first).
-int census_path_items(const Geom& g, int only_dir, int n_slots, int group, uint32_t* out, int cap)
+int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, uint32_t* out, int cap)
 {
     struct Item { int len; uint32_t code; };
     std::vector<Item> v;
     const PathLaunch16 pl = make_path_launch16(g);
     group = std::min(std::max(group, 1), kMaxGroup);
     for (int dir = 0; dir < 8; dir++) {
-        if (only_dir >= 0 && dir != only_dir) continue;
+        if (!((dir_mask >> dir) & 1u)) continue;
         if (dir >= 6) {
             const int nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
             for (int b = 0; b < nb; b++)
@@ -805,11 +850,16 @@ static void launch_paths_dpl(const PathFrames& pf, size_t vol_bytes, size_t tras
 
 // Path sweeps of the frames in pf (codes -> volumes). Each volume slice is vol_bytes long:
 // H*width1*D cells followed by a trash slot. items: device copy of census_path_items().
+// bnd_down / bnd_up (exact tile mode, may be null): see PathLaunch16.
 hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geom& g, const uint32_t* items,
-                               int n_items, hipStream_t st)
+                               int n_items, hipStream_t st, const uint8_t* bnd_down, const uint8_t* bnd_up,
+                               size_t bnd_slot)
 {
     if (n_items <= 0) return hipSuccess;
-    const PathLaunch16 pl = make_path_launch16(g);
+    PathLaunch16 pl = make_path_launch16(g);
+    pl.bnd[0] = bnd_down;
+    pl.bnd[1] = bnd_up;
+    pl.bnd_slot = bnd_slot;
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
     case 2: launch_paths_dpl<2>(pf, vol_bytes, trash_off, g, pl, items, n_items, st); break;

@@ -22,8 +22,9 @@
 
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
-int census_path_items(const Geom&, int, int, int, uint32_t*, int);
-hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t);
+int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int);
+hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t,
+                               const uint8_t* = nullptr, const uint8_t* = nullptr, size_t = 0);
 hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
 hipError_t launch_rectify_map(const double*, const double*, const double*, int, int, float*, float*, size_t,
                               hipStream_t);
@@ -133,6 +134,11 @@ struct sgm_handle {
     int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
     bool rect_on = false;          // sgm_set_rectification: batch inputs are raw, rectified in the census
     sgm::RectifyIn rect{};
+    // exact tile mode (sgm_match_tiled_exact): one handle per row band, each with a second
+    // stream for its upward sweeps and four events (census, down, up, gather)
+    std::vector<sgm_handle*> bands;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t bev[4] = {};
 };
 
 namespace {
@@ -259,10 +265,10 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
             l.vols[i] = take(l.vol_bytes * 8);
         }
         if (g.width1 > 0) {
-            l.n_items[0] = sgm::census_path_items(g, -1, 1, 1, nullptr, 0);
+            l.n_items[0] = sgm::census_path_items(g, 0xFFu, 1, 1, nullptr, 0);
             l.items[0] = take((size_t)l.n_items[0] * 4);
             if (group > 0) {
-                l.n_items[1] = sgm::census_path_items(g, -1, 1, l.group, nullptr, 0);
+                l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0);
                 l.items[1] = take((size_t)l.n_items[1] * 4);
             }
         }
@@ -307,15 +313,15 @@ struct StageRec {
 
 // Device work list of the census path launch for (g, only_dir), uploaded on `st` when the
 // geometry or the workspace changed. Returns the entry count (< 0: error).
-int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, int group, hipStream_t st,
+int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask, int group, hipStream_t st,
                const uint32_t** dev)
 {
     const int w = group > 1 ? 1 : 0;
     uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items[w]);
     *dev = d;
     char key[160];
-    snprintf(key, sizeof key, "%d %d %d %d %d %d %d %p", g.W, g.H, g.D, g.minD, only_dir, group, h->n_cu, (void*)d);
-    const int n = sgm::census_path_items(g, only_dir, h->n_cu, group, nullptr, 0);
+    snprintf(key, sizeof key, "%d %d %d %d %x %d %d %p", g.W, g.H, g.D, g.minD, dir_mask, group, h->n_cu, (void*)d);
+    const int n = sgm::census_path_items(g, dir_mask, h->n_cu, group, nullptr, 0);
     if (h->items_key[w] == key) return n;
     if (n > l.n_items[w]) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
     if (n > h->items_cap) {
@@ -325,7 +331,7 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, int only_dir, int 
         HIP_TRY(hipHostMalloc((void**)&h->items_pin, (size_t)n * 4, hipHostMallocDefault), "hipHostMalloc");
         h->items_cap = n;
     }
-    sgm::census_path_items(g, only_dir, h->n_cu, group, h->items_pin, h->items_cap);
+    sgm::census_path_items(g, dir_mask, h->n_cu, group, h->items_pin, h->items_cap);
     HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
     HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
     h->items_key[w] = key;
@@ -381,7 +387,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("census", 2 * WH + 16 * WH);
         HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
         const uint32_t* items;
-        const int n_items = path_items(h, l, g, -1, 1, st, &items);
+        const int n_items = path_items(h, l, g, 0xFFu, 1, st, &items);
         if (n_items < 0) return n_items;
         sgm::PathFrames pf{};
         pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
@@ -443,7 +449,7 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
     const int G = l.group;
     const int ng = (n + G - 1) / G;
     const uint32_t* items;
-    const int n_items = path_items(h, l, g, -1, G, st, &items);
+    const int n_items = path_items(h, l, g, 0xFFu, G, st, &items);
     if (n_items < 0) return n_items;
     StageRec rec{h};
     if (h->profiling) h->prof_frames += n;
@@ -581,8 +587,12 @@ void sgm_destroy(sgm_handle* h)
 {
     if (!h) return;
     for (sgm_handle* s : h->sub) sgm_destroy(s);
+    for (sgm_handle* s : h->bands) sgm_destroy(s);
     if (hipSetDevice(h->device) == hipSuccess) {
         if (h->stream) (void)hipStreamSynchronize(h->stream);
+        if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+        for (hipEvent_t e : h->bev) if (e) (void)hipEventDestroy(e);
+        if (h->stream2) (void)hipStreamDestroy(h->stream2);
         if (h->ws.base) (void)hipFree(h->ws.base);
         if (h->pin) (void)hipHostFree(h->pin);
         if (h->items_pin) (void)hipHostFree(h->items_pin);
@@ -929,6 +939,286 @@ int sgm_match_tiled(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
     });
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------------ exact tile mode ----
+// SURVEY §8(e) "single huge frame", exact mode. Band b (rows [c0, c1)) runs on its own
+// handle: census of its rows (+3 image rows of halo, so the codes equal the full frame's),
+// horizontal scans (band-local), then its downward sweeps continue the lines of band b-1
+// from band b-1's last volume row and its upward sweeps those of band b+1 from its first
+// row. The boundary rows (3 directions x width1 x D u8 per seam and sweep) move between
+// devices with hipMemcpyPeerAsync (xGMI); the two chains run top-down and bottom-up
+// concurrently (separate streams), so the frame's critical path is H row steps per sweep
+// direction, whatever the band count. The WTA of a band needs only its own rows.
+namespace {
+
+constexpr unsigned kDirsHoriz = 0xC0u, kDirsDown = 0x0Du, kDirsUp = 0x32u;
+
+struct BandLayout {
+    size_t inL = 0, inR = 0, cL = 0, cR = 0, vols = 0, vol_bytes = 0, items[3] = {}, bnd[2] = {}, bnd_slot = 0, raw = 0;
+    int n_items[3] = {};
+    size_t total = 0;
+};
+
+BandLayout make_band_layout(const Geom& g, int He)
+{
+    BandLayout l;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
+    const size_t w1 = (size_t)std::max(g.width1, 0);    // width1 <= 0: no paths, all invalid
+    const size_t cells = w1 * g.H * g.D;
+    l.inL = take((size_t)g.W * He);
+    l.inR = take((size_t)g.W * He);
+    l.cL = take((size_t)g.W * He * 8);
+    l.cR = take((size_t)g.W * He * 8);
+    l.vol_bytes = align_up(cells + kTrashBytes);
+    l.vols = take(l.vol_bytes * 8);
+    const unsigned masks[3] = {kDirsHoriz, kDirsDown, kDirsUp};
+    for (int i = 0; i < 3; i++) {
+        l.n_items[i] = w1 ? sgm::census_path_items(g, masks[i], 1, 1, nullptr, 0) : 0;
+        l.items[i] = take((size_t)l.n_items[i] * 4);
+    }
+    // + 512 B: lanes past D (D < 16 * DPL) read beyond the last pixel before being masked
+    l.bnd_slot = align_up(w1 * g.D + 512);
+    l.bnd[0] = take(3 * l.bnd_slot);
+    l.bnd[1] = take(3 * l.bnd_slot);
+    l.raw = take((size_t)g.W * g.H * 2);
+    l.total = off;
+    return l;
+}
+
+hipError_t copy_between(void* dst, int ddev, const void* src, int sdev, size_t n, hipStream_t st)
+{
+    return ddev == sdev ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st)
+                        : hipMemcpyPeerAsync(dst, ddev, src, sdev, n, st);
+}
+
+void enable_peer(int dev, int peer)
+{
+    if (dev == peer) return;
+    int ok = 0;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) return;
+    if (hipSetDevice(dev) != hipSuccess) return;
+    (void)hipDeviceEnablePeerAccess(peer, 0);    // already enabled: fine
+    (void)hipGetLastError();
+}
+
+// Stream 2 + events of a band handle; the three path work lists uploaded for g.
+int band_prepare(sgm_handle* b, const Geom& g, const BandLayout& l)
+{
+    sgm_handle* h = b;                            // for HIP_TRY
+    int rc = ensure_stream(b);
+    if (rc) return rc;
+    if (!b->stream2) HIP_TRY(hipStreamCreateWithFlags(&b->stream2, hipStreamNonBlocking), "hipStreamCreate");
+    for (hipEvent_t& e : b->bev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    if ((rc = ensure_ws(b, l.total))) return rc;
+    char key[160];
+    snprintf(key, sizeof key, "band %d %d %d %d %d %zu %p", g.W, g.H, g.D, g.minD, b->n_cu, l.total, b->ws.base);
+    if (b->items_key[0] == key) return SGM_OK;
+    const unsigned masks[3] = {kDirsHoriz, kDirsDown, kDirsUp};
+    std::vector<uint32_t> v;
+    for (int i = 0; i < 3 && g.width1 > 0; i++) {
+        const int n = sgm::census_path_items(g, masks[i], b->n_cu, 1, nullptr, 0);
+        if (n != l.n_items[i]) return fail(b, SGM_ERR_ARG, "band work list size mismatch");
+        v.resize(n);
+        sgm::census_path_items(g, masks[i], b->n_cu, 1, v.data(), n);
+        HIP_TRY(hipMemcpy((char*)b->ws.base + l.items[i], v.data(), (size_t)n * 4, hipMemcpyHostToDevice), "H2D items");
+    }
+    b->items_key[0] = key;
+    b->items_key[1].clear();
+    return SGM_OK;
+}
+
+// Post-filter workspace of the assembled frame on the primary handle.
+Layout make_post_layout(const sgm_params& p, const Geom& g)
+{
+    Layout l;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
+    const size_t WH = (size_t)g.W * g.H;
+    l.tmp = take(WH * 2);
+    l.out = take(WH * 2);
+    if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
+    l.total = off;
+    return l;
+}
+
+int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, int16_t* disp,
+                    size_t out_stride, int n_bands, const std::vector<int>& devs)
+{
+    const sgm_params& p = h->params;
+    Geom gf;
+    int rc = make_geom(p, W, H, gf, h->err);
+    if (rc) return rc;
+    if (p.mode != SGM_MODE_CENSUS8) return fail(h, SGM_ERR_UNSUPPORTED, "the exact tile mode runs in the census mode");
+    const int nb = n_bands;
+    while ((int)h->bands.size() < nb) h->bands.push_back(nullptr);
+    std::vector<int> c(nb + 1);
+    for (int b = 0; b <= nb; b++) c[b] = (int)((long long)b * H / nb);
+    std::vector<Geom> g(nb);
+    std::vector<BandLayout> bl(nb);
+    for (int b = 0; b < nb; b++) {
+        const int dev = devs[b % devs.size()];
+        sgm_handle*& bh = h->bands[b];
+        if (bh && bh->device != dev) { sgm_destroy(bh); bh = nullptr; }
+        if (!bh && (rc = sgm_create(&bh, dev))) return fail(h, rc, "cannot open device " + std::to_string(dev));
+        bh->params = p;
+        if ((rc = make_geom(p, W, c[b + 1] - c[b], g[b], h->err))) return rc;
+        const int e0 = std::max(0, c[b] - 3), e1 = std::min(H, c[b + 1] + 3);
+        bl[b] = make_band_layout(g[b], e1 - e0);
+        if ((rc = band_prepare(bh, g[b], bl[b]))) return fail(h, rc, "band " + std::to_string(b) + ": " + bh->err);
+        if ((rc = ensure_pin(bh, 2 * (size_t)W * (e1 - e0)))) return fail(h, rc, bh->err);
+    }
+    for (int b = 0; b < nb; b++) {
+        if (b > 0) enable_peer(h->bands[b]->device, h->bands[b - 1]->device);
+        if (b + 1 < nb) enable_peer(h->bands[b]->device, h->bands[b + 1]->device);
+        enable_peer(h->bands[b]->device, h->device);
+    }
+    if ((rc = ensure_stream(h))) return rc;
+    const Layout pl = make_post_layout(p, gf);
+    if ((rc = ensure_ws(h, pl.total))) return rc;
+    if ((rc = ensure_pin(h, (size_t)W * H * 2))) return rc;
+    const bool med = use_median(p);
+    char* pws = (char*)h->ws.base;
+    int16_t* frame_raw = (int16_t*)(pws + (med ? pl.tmp : pl.out));
+    const size_t cells_row = (size_t)std::max(gf.width1, 0) * gf.D;
+
+    auto ws = [&](int b, size_t off) { return (char*)h->bands[b]->ws.base + off; };
+    auto fail_band = [&](int b, hipError_t e, const char* where) {
+        for (sgm_handle* s : h->bands)
+            if (s && s->stream) { (void)hipSetDevice(s->device); (void)hipStreamSynchronize(s->stream);
+                                   (void)hipStreamSynchronize(s->stream2); }
+        return fail(h, SGM_ERR_DEVICE, "band " + std::to_string(b) + " " + where + ": " + hipGetErrorString(e));
+    };
+#define BAND_TRY(b, expr, where)                          \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return fail_band(b, e_, where); \
+    } while (0)
+    enum { EV_CENSUS = 0, EV_DOWN = 1, EV_UP = 2, EV_GATHER = 3 };
+    // 1. inputs, census, horizontal scans (band-local)
+    for (int b = 0; b < nb; b++) {
+        sgm_handle* bh = h->bands[b];
+        BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+        const int e0 = std::max(0, c[b] - 3), e1 = std::min(H, c[b + 1] + 3), He = e1 - e0;
+        const size_t n = (size_t)W * He;
+        for (int y = 0; y < He; y++) {
+            std::memcpy(bh->pin + (size_t)y * W, L + (size_t)(e0 + y) * stride, W);
+            std::memcpy(bh->pin + n + (size_t)y * W, R + (size_t)(e0 + y) * stride, W);
+        }
+        BAND_TRY(b, hipMemcpyAsync(ws(b, bl[b].inL), bh->pin, n, hipMemcpyHostToDevice, bh->stream), "H2D");
+        BAND_TRY(b, hipMemcpyAsync(ws(b, bl[b].inR), bh->pin + n, n, hipMemcpyHostToDevice, bh->stream), "H2D");
+        BAND_TRY(b, sgm::launch_census((const uint8_t*)ws(b, bl[b].inL), (const uint8_t*)ws(b, bl[b].inR), W, W, He,
+                                       (uint64_t*)ws(b, bl[b].cL), (uint64_t*)ws(b, bl[b].cR), bh->stream), "census");
+        BAND_TRY(b, hipEventRecord(bh->bev[EV_CENSUS], bh->stream), "event");
+    }
+    auto frames = [&](int b) {
+        sgm::PathFrames pf{};
+        const size_t skip = (size_t)(c[b] - std::max(0, c[b] - 3)) * W;   // codes of the band's first row
+        pf.cL[0] = (const uint64_t*)ws(b, bl[b].cL) + skip;
+        pf.cR[0] = (const uint64_t*)ws(b, bl[b].cR) + skip;
+        pf.vols[0] = (uint8_t*)ws(b, bl[b].vols);
+        pf.n = 1;
+        return pf;
+    };
+    if (gf.width1 > 0) {
+        for (int b = 0; b < nb; b++) {
+            sgm_handle* bh = h->bands[b];
+            BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+            BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[0]),
+                                                 bl[b].n_items[0], bh->stream), "horizontal paths");
+        }
+        // 2. downward chain, top to bottom: band b continues band b-1's last row
+        static const int down_dirs[3] = {0, 2, 3}, up_dirs[3] = {1, 4, 5};
+        for (int b = 0; b < nb; b++) {
+            sgm_handle* bh = h->bands[b];
+            BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+            if (b > 0) BAND_TRY(b, hipStreamWaitEvent(bh->stream, h->bands[b - 1]->bev[EV_DOWN], 0), "wait");
+            BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[1]),
+                                                 bl[b].n_items[1], bh->stream,
+                                                 b > 0 ? (const uint8_t*)ws(b, bl[b].bnd[0]) : nullptr, nullptr,
+                                                 bl[b].bnd_slot), "down paths");
+            if (b + 1 < nb) {
+                const size_t last = (size_t)(g[b].H - 1) * cells_row;
+                for (int k = 0; k < 3; k++)
+                    BAND_TRY(b, copy_between(ws(b + 1, bl[b + 1].bnd[0] + k * bl[b + 1].bnd_slot), h->bands[b + 1]->device,
+                                             ws(b, bl[b].vols + down_dirs[k] * bl[b].vol_bytes + last), bh->device,
+                                             cells_row, bh->stream), "boundary copy");
+            }
+            BAND_TRY(b, hipEventRecord(bh->bev[EV_DOWN], bh->stream), "event");
+        }
+        // 3. upward chain, bottom to top, on the second streams: band b continues band b+1's first row
+        for (int b = nb - 1; b >= 0; b--) {
+            sgm_handle* bh = h->bands[b];
+            BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+            BAND_TRY(b, hipStreamWaitEvent(bh->stream2, bh->bev[EV_CENSUS], 0), "wait");
+            if (b + 1 < nb) BAND_TRY(b, hipStreamWaitEvent(bh->stream2, h->bands[b + 1]->bev[EV_UP], 0), "wait");
+            BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[2]),
+                                                 bl[b].n_items[2], bh->stream2, nullptr,
+                                                 b + 1 < nb ? (const uint8_t*)ws(b, bl[b].bnd[1]) : nullptr,
+                                                 bl[b].bnd_slot), "up paths");
+            if (b > 0)
+                for (int k = 0; k < 3; k++)
+                    BAND_TRY(b, copy_between(ws(b - 1, bl[b - 1].bnd[1] + k * bl[b - 1].bnd_slot), h->bands[b - 1]->device,
+                                             ws(b, bl[b].vols + up_dirs[k] * bl[b].vol_bytes), bh->device, cells_row,
+                                             bh->stream2), "boundary copy");
+            BAND_TRY(b, hipEventRecord(bh->bev[EV_UP], bh->stream2), "event");
+        }
+    }
+    // 4. WTA of each band (after its three path launches), gathered into the primary's frame
+    for (int b = 0; b < nb; b++) {
+        sgm_handle* bh = h->bands[b];
+        BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+        int16_t* raw = (int16_t*)ws(b, bl[b].raw);
+        if (gf.width1 > 0) {
+            BAND_TRY(b, hipStreamWaitEvent(bh->stream, bh->bev[EV_UP], 0), "wait");
+            sgm::WtaFrames wf{};
+            wf.vols[0] = (const uint8_t*)ws(b, bl[b].vols); wf.out[0] = raw; wf.n = 1;
+            BAND_TRY(b, sgm::launch_census_wta(wf, bl[b].vol_bytes, g[b], W, bh->stream), "wta");
+        } else {
+            BAND_TRY(b, sgm::launch_fill16(raw, W, W, g[b].H, gf.invalid, bh->stream), "fill");
+        }
+        BAND_TRY(b, copy_between(frame_raw + (size_t)c[b] * W, h->device, raw, bh->device, (size_t)W * g[b].H * 2,
+                                 bh->stream), "gather");
+        BAND_TRY(b, hipEventRecord(bh->bev[EV_GATHER], bh->stream), "event");
+    }
+#undef BAND_TRY
+    // 5. post filters on the assembled frame (median / speckles need no band seams), D2H
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    for (int b = 0; b < nb; b++) HIP_TRY(hipStreamWaitEvent(h->stream, h->bands[b]->bev[EV_GATHER], 0), "wait");
+    StageRec rec{h};
+    int16_t* out = (int16_t*)(pws + pl.out);
+    if ((rc = run_post(h, pl, gf, out, W, rec))) return rc;
+    rec.end();
+    HIP_TRY(hipMemcpyAsync(h->pin, out, (size_t)W * H * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    const int16_t* src = (const int16_t*)h->pin;
+    for (int y = 0; y < H; y++) std::memcpy(disp + (size_t)y * out_stride, src + (size_t)y * W, 2 * (size_t)W);
+    return SGM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sgm_match_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride,
+                          int16_t* disp, size_t out_stride, int n_bands, const int* devices, int n_dev)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W || n_bands < 1)
+        return fail(h, SGM_ERR_ARG, "bad buffers, sizes or band count");
+    std::vector<int> devs;
+    if (!devices || n_dev <= 0) {
+        for (int i = 0; i < sgm_device_count(); i++) devs.push_back(i);
+    } else {
+        devs.assign(devices, devices + n_dev);
+    }
+    if (devs.empty()) return fail(h, SGM_ERR_DEVICE, "no HIP device");
+    std::lock_guard<std::mutex> lk(h->mu);
+    return run_tiled_exact(h, L, R, W, H, stride, disp, out_stride, std::min(n_bands, H), devs);
+}
+
 int sgm_set_profiling(sgm_handle* h, int enable)
 {
     if (!h) return SGM_ERR_ARG;
@@ -1023,7 +1313,7 @@ int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int
     HIP_TRY(sgm::launch_census((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, W, H, cL, cR, h->stream),
             "census");
     const uint32_t* items;
-    const int n_items = path_items(h, l, g, dir, 1, h->stream, &items);
+    const int n_items = path_items(h, l, g, 1u << dir, 1, h->stream, &items);
     if (n_items < 0) return n_items;
     sgm::PathFrames pf{};
     pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;

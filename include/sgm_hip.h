@@ -123,6 +123,19 @@ int  sgm_match_tiled(sgm_handle* h, const uint8_t* left, const uint8_t* right, i
                      size_t stride, int16_t* disp, size_t out_stride, int n_bands, int halo,
                      const int* devices, int n_dev);
 
+/* The same band split in exact mode (SURVEY §8(e) "exact mode", census mode only): band b
+ * continues the path lines of its neighbours. Its downward sweeps start from the last
+ * volume row of band b-1 and its upward sweeps from the first row of band b+1. Those
+ * boundary rows (3 directions x width1 x D u8 per seam) move device to device with
+ * hipMemcpyPeerAsync (xGMI). The top-down and bottom-up chains run concurrently; the WTA of a
+ * band uses only its own rows, and median/speckle filters run on the assembled frame on h's
+ * device. The result is bit-identical to sgm_match for any band count. Host buffers;
+ * synchronous. Replaces nothing in the reference (no reference tile mode exists); the
+ * per-frame contract is that of cv::StereoSGBM::compute (matcherOpenCVSGBM.cpp:21).       */
+int  sgm_match_tiled_exact(sgm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                           size_t stride, int16_t* disp, size_t out_stride, int n_bands,
+                           const int* devices, int n_dev);
+
 /* Frame batch on device buffers (host arrays of n_frames device pointers), asynchronous on
  * `stream`. Census mode pipelines the frames: the path aggregation of frame i+1 and the
  * WTA of frame i run in ONE launch (VALU-bound and HBM-bound work side by side), with two

@@ -266,3 +266,62 @@ def test_c5_tiled_vs_full_frame(engine, synth, pkg):
     print(f"C5 8 bands, halo 128: {100 * frac:.4f} % of pixels differ from the full frame")
     assert frac < 0.001
     assert (full != -16).mean() > 0.5
+
+
+EXACT_CASES = [
+    (dict(num_disparities=64), 2),
+    (dict(num_disparities=64), 5),
+    (dict(num_disparities=48, min_disparity=2), 3),        # D < 16*DPL: masked lanes in the seed
+    (dict(num_disparities=32, min_disparity=-9), 4),       # negative minD (maxX1 < W)
+    (dict(num_disparities=128, median=1, speckle_window_size=30, speckle_range=2), 4),  # post on the frame
+    (dict(num_disparities=256, uniqueness_ratio=0), 3),
+    (dict(num_disparities=400, min_disparity=3), 2),       # DPL 32, lane straddling D
+    (dict(num_disparities=64), 61),                        # one-row bands
+]
+
+
+@pytest.mark.parametrize("kw,bands", EXACT_CASES, ids=[str(i) for i in range(len(EXACT_CASES))])
+def test_tiled_exact_equals_full_frame(engine, oracle, synth, pkg, kw, bands):
+    """SURVEY §8(e) exact mode: path lines continue across band seams through the
+    boundary-row exchange, so every band count gives the full-frame result bit for bit."""
+    D, minD = kw["num_disparities"], kw.get("min_disparity", 0)
+    h, w = 61, max(D + minD, 0) + 133
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=D + bands)
+    p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
+    engine.set_params(p)
+    got = engine.match_tiled_exact(left, right, bands)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+def test_tiled_exact_band_devices_and_reuse(engine, oracle, synth, pkg):
+    """Bands dealt over an explicit device list (all device 0 here, the 8-GPU layout of
+    C5 on one card), the band handles reused across calls and geometry changes."""
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    op = to_oracle_params(oracle, p)
+    for (h, w, bands, seed) in [(96, 256, 8, 3), (40, 200, 3, 4), (96, 256, 8, 5)]:
+        left, right, _ = synth.stereo_pair(h, w, 0, 64, seed=seed)
+        got = engine.match_tiled_exact(left, right, bands, devices=[0] * 8)
+        assert np.array_equal(got, oracle.match(op, left, right)), (h, w, bands)
+
+
+def test_tiled_exact_no_disparity_window(engine, pkg):
+    """width1 <= 0 (D wider than the image): every pixel invalid, as in sgm_match."""
+    left = np.full((20, 40), 9, np.uint8)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
+    engine.set_params(p)
+    got = engine.match_tiled_exact(left, left, 3)
+    assert np.array_equal(got, engine.match(left, left))
+    assert (got == -16).all()
+
+
+def test_c5_tiled_exact_vs_full_frame(engine, synth, pkg):
+    """BASELINE config C5 (4096x3000, D=512) in exact mode: 8 bands with boundary-row
+    exchange equal the single-device full frame at every pixel."""
+    h, w, D = 3000, 4096, 512
+    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=5, with_truth=False)
+    engine.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D))
+    full = engine.match(left, right)
+    tiled = engine.match_tiled_exact(left, right, 8)
+    assert np.array_equal(tiled, full), f"{(tiled != full).sum()} pixels differ"
