@@ -11,6 +11,16 @@
 // stored); S never touches HBM.
 #include "sgm_device.h"
 
+#ifndef SGM_WPE
+#define SGM_WPE 4          // minimum waves per SIMD of the path kernels (register budget)
+#endif
+#ifndef SGM_SEG_UNCLAMPED
+#define SGM_SEG_UNCLAMPED 1
+#endif
+#ifndef SGM_ROWS_PRELOAD
+#define SGM_ROWS_PRELOAD 0
+#endif
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -143,6 +153,32 @@ __device__ __forceinline__ uint32_t ham_acc(uint64_t a, uint64_t b, uint32_t acc
 {
     const uint64_t x = a ^ b;
     return bcnt_acc((uint32_t)(x >> 32), bcnt_acc((uint32_t)x, acc));
+}
+
+// packed u16 helpers of the WTA: per-half shift and saturating subtract
+__device__ __forceinline__ uint32_t pk_shl(uint32_t a, int sh)
+{
+    return as_u(as_v2(a) << (u16x2_t){(unsigned short)sh, (unsigned short)sh});
+}
+__device__ __forceinline__ uint32_t pk_subs(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_sub_sat(as_v2(a), as_v2(b))); }
+// sum over the 16 lanes of each row, result in every lane of the row
+__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);    // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true);    // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, true);   // row_ror:4
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, true);   // row_ror:8
+    return v;
+}
+// C-style truncating num / den (|num| < 2^24, den > 0) from the hardware reciprocal: the
+// estimate is within one of the quotient, then fixed like tdiv()
+__device__ __forceinline__ int tdiv_rcp(int num, int den)
+{
+    int q = (int)__builtin_truncf((float)num * __builtin_amdgcn_rcpf((float)den));
+    const int r = num - q * den;
+    if (num >= 0) q += (r >= den) ? 1 : (r < 0 ? -1 : 0);
+    else          q += (r <= -den) ? -1 : (r > 0 ? 1 : 0);
+    return q;
 }
 
 // Relative state of a line from its absolute costs: Lr = Labs - min over the row's D
@@ -346,6 +382,43 @@ __device__ __forceinline__ void seg_load(uint64_t (&v)[RowSeg<DPL>::NLOAD], cons
     }
 }
 
+// Unclamped form: the code images have kCodeMargin readable codes before and after them
+// (workspace layout), and the codes outside [0, W) of a row feed only lines or lanes whose
+// results go to the trash slot, so each lane keeps ONE byte offset for the whole sweep and a
+// step moves the wave-uniform base (SGPR base + VGPR offset loads, no per-step VALU).
+template <int DPL>
+struct SegAddr {
+    uint32_t off[RowSeg<DPL>::NLOAD];   // byte offsets from the step base
+    const char* lo;                     // min(cL, cR) - bias codes
+    int bias;
+};
+template <int DPL>
+__device__ __forceinline__ SegAddr<DPL> seg_addr(const uint64_t* cL, const uint64_t* cR, const Geom& g, int tid)
+{
+    using RS = RowSeg<DPL>;
+    SegAddr<DPL> a;
+    const uint64_t* base = cL < cR ? cL : cR;
+    a.bias = 16 * DPL + max(g.minD, 0);                 // makes every lane offset >= 0
+    a.lo = (const char*)base - (size_t)8 * a.bias;
+#pragma unroll
+    for (int m = 0; m < RS::NLOAD; m++) {
+        const int q = min(tid + m * kWG, RS::NTOT - 1);
+        const int rel = q < RS::NSEG ? (int)(cR - base) + q - g.minD - 16 * DPL + 1 : (int)(cL - base) + (q - RS::NSEG);
+        a.off[m] = (uint32_t)(8 * (rel + a.bias));
+    }
+    return a;
+}
+template <int DPL>
+__device__ __forceinline__ void seg_load_u(uint64_t (&v)[RowSeg<DPL>::NLOAD], const SegAddr<DPL>& a, const Geom& g,
+                                           int rx, int ry, int xb, int s)
+{
+    const int y = ry > 0 ? s : g.H - 1 - s;
+    const int yc = min(max(y, 0), g.H - 1);
+    const char* sb = a.lo + (size_t)8 * ((size_t)yc * g.W + (xb + rx * s));   // wave-uniform
+#pragma unroll
+    for (int m = 0; m < RowSeg<DPL>::NLOAD; m++) v[m] = *(const uint64_t*)(sb + a.off[m]);
+}
+
 template <int DPL>
 __device__ __forceinline__ void seg_store(uint64_t* buf, const uint64_t (&v)[RowSeg<DPL>::NLOAD], int tid)
 {
@@ -423,11 +496,17 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     uint64_t* buf0 = lds;
     uint64_t* buf1 = lds + RS::BUF;
     uint64_t R0[RS::NLOAD], R1[RS::NLOAD], R2[RS::NLOAD], R3[RS::NLOAD];
-    seg_load<DPL>(R0, cL, cR, g, rx, ry, xb, s0, tid);
+#if SGM_SEG_UNCLAMPED
+    const SegAddr<DPL> sa = seg_addr<DPL>(cL, cR, g, tid);
+#define SEG_LOAD(R, st) seg_load_u<DPL>(R, sa, g, rx, ry, xb, st)
+#else
+#define SEG_LOAD(R, st) seg_load<DPL>(R, cL, cR, g, rx, ry, xb, st, tid)
+#endif
+    SEG_LOAD(R0, s0);
     seg_store<DPL>(buf0, R0, tid);
-    seg_load<DPL>(R1, cL, cR, g, rx, ry, xb, min(s0 + 1, s1 - 1), tid);
-    seg_load<DPL>(R2, cL, cR, g, rx, ry, xb, min(s0 + 2, s1 - 1), tid);
-    seg_load<DPL>(R3, cL, cR, g, rx, ry, xb, min(s0 + 3, s1 - 1), tid);
+    SEG_LOAD(R1, min(s0 + 1, s1 - 1));
+    SEG_LOAD(R2, min(s0 + 2, s1 - 1));
+    SEG_LOAD(R3, min(s0 + 3, s1 - 1));
     __syncthreads();
 
     auto step = [&](int s, const uint64_t* bufc) {
@@ -439,7 +518,15 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         // path start (first valid pixel of the line): L = C. The P2 cap of the recurrence is
         // lowered to "0" (kBase), which clamps every candidate: one select per step.
         const uint32_t P2x = pv ? P2P2 : kBaseP2;
+#if SGM_ROWS_PRELOAD
+        uint64_t crv[DPL];
+#pragma unroll
+        for (int k = 0; k < DPL; k++) crv[k] = bufc[RS::phys(e_hi - k)];
+        __builtin_amdgcn_sched_barrier(0);
+        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return crv[k]; }, P1P1, P2x, imask, Labs);
+#else
         p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
+#endif
         const bool ok = valid && lane_act;
         uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
         uint8_t* const dst = ok ? vrow + (uint32_t)((x - g.minX1) * g.D + p * DPL) : tr;
@@ -450,7 +537,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     // (s + 1) % 4) goes to buf[(s + 1) & 1] and set s % 4 is reloaded with segment s + 4
     auto body = [&](int s, const uint64_t* bcur, uint64_t* bnext, uint64_t (&Rnext)[RS::NLOAD],
                     uint64_t (&Rfree)[RS::NLOAD]) {
-        seg_load<DPL>(Rfree, cL, cR, g, rx, ry, xb, min(s + 4, s1 - 1), tid);
+        SEG_LOAD(Rfree, min(s + 4, s1 - 1));
         step(s, bcur);
         seg_store<DPL>(bnext, Rnext, tid);
         __syncthreads();
@@ -461,6 +548,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         body(s + 2, buf0, buf1, R3, R2);
         body(s + 3, buf1, buf0, R0, R3);
     }
+#undef SEG_LOAD
 }
 
 // One work-list entry: 16 lines of one direction of one frame (lds: 2 * RowSeg<DPL>::BUF).
@@ -493,7 +581,7 @@ __device__ __forceinline__ void trace_record(uint64_t* trace, uint64_t tag, uint
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : SGM_WPE)))
 void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
                       const uint32_t* __restrict__ items, uint64_t* __restrict__ trace)
 {
@@ -521,7 +609,8 @@ void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g,
 template <int DPL>
 __host__ __device__ constexpr size_t wta_key_bytes(int W)
 {
-    return (size_t)kWG * DPL * 2 > (size_t)4 * W ? (size_t)kWG * DPL * 2 : (size_t)4 * W;
+    // per lane 2 * NWD dwords of packed S (NWD = (DPL + 3) / 4)
+    return (size_t)kWG * 8 * ((DPL + 3) / 4) > (size_t)4 * W ? (size_t)kWG * 8 * ((DPL + 3) / 4) : (size_t)4 * W;
 }
 template <int DPL>
 __host__ __device__ constexpr size_t wta_lds_bytes(int W) { return wta_key_bytes<DPL>(W) + RowLds::rest_bytes(W); }
@@ -532,7 +621,7 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
                                           int16_t* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
 {
     constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
-    uint32_t* sl = lds;                           // 4 waves x 4 rows x 16*DPL u16 S values
+    uint32_t* sl = lds;                           // 4 waves x 4 rows x 16 lanes x 2*NWD packed S dwords
     RowLds R(lds, (char*)lds + wta_key_bytes<DPL>(g.W), g.W);   // R.key aliases sl
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane >> 4, p = lane & 15;
@@ -542,7 +631,18 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     // SGPR-base + VGPR-offset addressing
     const size_t row0 = (size_t)y * g.width1 * g.D;
     const uint32_t off0 = (uint32_t)(lane_act ? p * DPL : 0);
-    uint32_t* srow = sl + (w * 4 + r) * 8 * DPL;
+    uint32_t* srow = sl + (w * 4 + r) * 32 * NWD;     // 16 lanes x 2 * NWD dwords
+    // packed-key geometry: lane-local index k in the low KB bits of a 16-bit key
+    constexpr int KB = DPL > 16 ? 5 : 4;
+    constexpr uint32_t KMASK = (1u << KB) - 1;
+    uint32_t emaskE[NWD], emaskO[NWD];            // 0xFFFF in halves with k >= DPL or d >= D
+#pragma unroll
+    for (int j = 0; j < NWD; j++) {
+        auto bad = [&](int k) { return k >= DPL || (!EXACT && p * DPL + k >= g.D); };
+        emaskE[j] = (bad(4 * j) ? 0xFFFFu : 0u) | (bad(4 * j + 2) ? 0xFFFF0000u : 0u);
+        emaskO[j] = (bad(4 * j + 1) ? 0xFFFFu : 0u) | (bad(4 * j + 3) ? 0xFFFF0000u : 0u);
+    }
+    const float inv_u = 1.0f / (float)max(100 - g.uniq, 1);
     const int n = g.width1;
     const int nq = (n + 3) / 4;
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
@@ -550,60 +650,81 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
 #pragma unroll
         for (int vv = 0; vv < 8; vv++) wload<DPL>(vols + (size_t)vv * vol_bytes + row0 + off, v[vv]);
     };
-    uint32_t cur[8][NWD], nxt[8][NWD];
-    load(min(w, nq - 1), cur);
-    for (int q = w; q < nq; q += 4) {
-        load(min(q + 4, nq - 1), nxt);
-        // ---- S in u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]) ----
-        uint32_t E[NWD], O[NWD];
+    // S in u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]); halves past D or past
+    // the lane's DPL are 0xFFFF. The next pixel group's loads are summed at the end of an
+    // iteration, so only one set of raw volume words is live.
+    uint32_t E[NWD], O[NWD];
+    auto sum8 = [&](const uint32_t (&v)[8][NWD]) {
 #pragma unroll
         for (int j = 0; j < NWD; j++) {
             uint32_t e = 0, o = 0;
 #pragma unroll
             for (int vv = 0; vv < 8; vv++) {
-                e += cur[vv][j] & 0x00FF00FFu;
-                o += __builtin_amdgcn_perm(0u, cur[vv][j], 0x0c030c01u);
+                e += v[vv][j] & 0x00FF00FFu;
+                o += __builtin_amdgcn_perm(0u, v[vv][j], 0x0c030c01u);
             }
-            E[j] = e;
-            O[j] = o;
+            E[j] = e | emaskE[j];
+            O[j] = o | emaskO[j];
         }
-        // ---- keys, min -> (minS, best) ----
-        uint32_t S[4 * NWD], key[4 * NWD];
-        uint32_t kmin = 0xFFFFFFFFu;
+    };
+    uint32_t nxt[8][NWD];
+    load(min(w, nq - 1), nxt);
+    sum8(nxt);
+    for (int q = w; q < nq; q += 4) {
+        load(min(q + 4, nq - 1), nxt);
+        // ---- (minS, best): packed 16-bit keys S << KB | k, one 16-lane min over S*512 + d ----
+        uint32_t km = 0xFFFFFFFFu;
 #pragma unroll
         for (int j = 0; j < NWD; j++) {
-            S[4 * j + 0] = E[j] & 0xFFFFu; S[4 * j + 2] = E[j] >> 16;
-            S[4 * j + 1] = O[j] & 0xFFFFu; S[4 * j + 3] = O[j] >> 16;
+            const uint32_t ke = pk_shl(E[j], KB) | (((uint32_t)(4 * j + 2) << 16) | (uint32_t)(4 * j));
+            const uint32_t ko = pk_shl(O[j], KB) | (((uint32_t)(4 * j + 3) << 16) | (uint32_t)(4 * j + 1));
+            km = pk_min(km, pk_min(ke, ko));
         }
-#pragma unroll
-        for (int k = 0; k < DPL; k++) {
-            const int d = p * DPL + k;
-            if (!EXACT && d >= g.D) S[k] = 0xFFFFu;
-            key[k] = (S[k] << 9) | (uint32_t)(d & 511);
-            kmin = min(kmin, key[k]);
-        }
-        kmin = row_min_u32(kmin);
+        km = pk_min(km, alignbit16(km, km)) & 0xFFFFu;      // lane min key (low half)
+        const uint32_t kmin = row_min_u32(((km >> KB) << 9) | (uint32_t)(p * DPL + (int)(km & KMASK)));
         const int best = (int)(kmin & 511u);
         const int minS = (int)(kmin >> 9);
-        // ---- uniqueness: min S over d outside [best-1, best+1] ----
-        uint32_t k2 = 0xFFFFFFFFu;
+        // ---- the row's packed S slice in LDS (S[best +- 1] for subpixel and uniqueness) ----
 #pragma unroll
-        for (int k = 0; k < DPL; k++) {
-            const int d = p * DPL + k;
-            k2 = ((unsigned)(d - best + 1) <= 2u || (!EXACT && d >= g.D)) ? k2 : min(k2, key[k]);
+        for (int j = 0; j < NWD; j++) { srow[p * 2 * NWD + j] = E[j]; srow[p * 2 * NWD + NWD + j] = O[j]; }
+        auto s_at = [&](int d) {
+            const int kk = d % DPL;
+            const uint32_t v = srow[(d / DPL) * 2 * NWD + (kk & 1) * NWD + (kk >> 2)];
+            return (int)((v >> (16 * ((kk >> 1) & 1))) & 0xFFFFu);
+        };
+        const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, 16 * DPL - 1));
+        // ---- uniqueness: reject if some d outside [best-1, best+1] has S*(100-u) < minS*100.
+        // For u < 100 that is S <= thr = (minS*100 - 1) / (100 - u); with T = thr + 1 the sum of
+        // max(T - S, 0) over the row exceeds its window part exactly when such a d exists. For
+        // u >= 100 every d qualifies when minS > 0, and for u > 100, minS == 0 those with S > 0
+        // (the count of S == 0 outside the window is the same sum with T = 1).
+        int T = 0;
+        if (g.uniq < 100) {
+            if (minS > 0) {
+                const int num = minS * 100 - 1, den = 100 - g.uniq;
+                int q = (int)((float)num * inv_u);
+                q += (q + 1) * den <= num ? 1 : 0;
+                q -= q * den > num ? 1 : 0;
+                T = min(q + 1, 8 * 255 + 1);      // S <= 8 * 255: keeps the u16 sums exact
+            }
+        } else {
+            T = (minS == 0 && g.uniq > 100) ? 1 : 0;
         }
-        k2 = row_min_u32(k2);
-        const bool rej = k2 != 0xFFFFFFFFu && (int)(k2 >> 9) * (100 - g.uniq) < minS * 100;
-        // ---- subpixel: S[best-1], S[best+1] through the row's LDS slice ----
-        // (one access type, u32, for the stores and the loads: no type-based reordering)
+        const uint32_t TT = (uint32_t)T * 0x10001u;
+        uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < DPL; k += 2) srow[(p * DPL + k) >> 1] = (S[k + 1] << 16) | S[k];
-        const int bm = max(best - 1, 0), bp = min(best + 1, 16 * DPL - 1);
-        const int sm = (int)((srow[bm >> 1] >> ((bm & 1) * 16)) & 0xFFFFu);
-        const int sp = (int)((srow[bp >> 1] >> ((bp & 1) * 16)) & 0xFFFFu);
+        for (int j = 0; j < NWD; j++) acc = pk_add(acc, pk_add(pk_subs(TT, E[j]), pk_subs(TT, O[j])));
+        const int tot = (int)row_sum_u32(__builtin_amdgcn_sad_u16(acc, 0u, 0u));
+        const int win = max(T - minS, 0) + (best > 0 ? max(T - sm, 0) : 0) + (best < g.D - 1 ? max(T - sp, 0) : 0);
+        int outside = tot - win;
+        if (g.uniq >= 100) {
+            const int nwin = 1 + (best > 0 ? 1 : 0) + (best < g.D - 1 ? 1 : 0);
+            outside = minS > 0 ? g.D - nwin : (g.uniq > 100 ? (g.D - nwin) - outside : 0);
+        }
+        const bool rej = outside > 0;
         const int den = max(sm + sp - 2 * minS, 1);
         const bool use = g.subpix && best > 0 && best < g.D - 1;
-        const int d16 = best * 16 + (use ? tdiv((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
         // ---- results: lane 0 of each row writes its pixel, the others hit dummy slots ----
         const int x1 = 4 * q + r;
         const bool wr = p == 0 && x1 < n;
@@ -611,10 +732,7 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
         R.bst[x] = (int16_t)(rej ? -1 : best);
         R.mins[x] = (uint16_t)minS;
         R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
-#pragma unroll
-        for (int vv = 0; vv < 8; vv++)
-#pragma unroll
-            for (int j = 0; j < NWD; j++) cur[vv][j] = nxt[vv][j];
+        sum8(nxt);
     }
     R.init_key(g, tid, kWG);                      // the S slices are dead: key takes their space
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
@@ -712,7 +830,7 @@ __global__ __launch_bounds__(kWG) void k_census_tiles(CensusFrames cf, int W, in
 
 // blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : 4)))
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : SGM_WPE)))
 void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_bytes, size_t trash_off, Geom g,
                       PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride,
                       int period16, uint64_t* __restrict__ trace)
@@ -798,10 +916,17 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
     if (n > cap) return -1;
     std::stable_sort(v.begin(), v.end(), [](const Item& a, const Item& b) { return a.len > b.len; });
     n_slots = std::max(n_slots, 1);
+    // XCD-aware placement (SGM_XCD_DEAL=1): blocks are dealt round-robin over the 8 XCDs, so
+    // slot j of a full round goes to block (j % per) * 8 + j / per: runs of `per` consecutive
+    // items (adjacent column blocks of one direction, whose row segments overlap) share an XCD
+    // and its L2.
+    static const int xcd = getenv("SGM_XCD_DEAL") ? atoi(getenv("SGM_XCD_DEAL")) : 0;
     for (int k = 0; k < n; k++) {
         const int round = k / n_slots, i = k % n_slots;
         const int in_round = std::min(n_slots, n - round * n_slots);
-        out[round * n_slots + ((round & 1) ? in_round - 1 - i : i)] = v[k].code;
+        int pos = (round & 1) ? in_round - 1 - i : i;
+        if (xcd && in_round == n_slots && n_slots % 8 == 0) pos = (pos % (n_slots / 8)) * 8 + pos / (n_slots / 8);
+        out[round * n_slots + pos] = v[k].code;
     }
     return n;
 }

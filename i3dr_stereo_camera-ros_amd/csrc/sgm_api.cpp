@@ -253,6 +253,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     Layout l;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 1)); return o; };
+    auto take_codes = [&](size_t n) { return take((n + 2 * sgm::kCodeMargin) * 8) + 8 * sgm::kCodeMargin; };
     const size_t WH = (size_t)g.W * g.H;
     const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
     if (p.mode == SGM_MODE_CENSUS8) {
@@ -260,8 +261,8 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.group = std::max(group, 1);
         const int sets = group > 0 ? 2 * l.group : 1;
         for (int i = 0; i < sets; i++) {
-            l.cL[i] = take(WH * 8);
-            l.cR[i] = take(WH * 8);
+            l.cL[i] = take_codes(WH);
+            l.cR[i] = take_codes(WH);
             l.vols[i] = take(l.vol_bytes * 8);
         }
         if (g.width1 > 0) {
@@ -969,8 +970,9 @@ BandLayout make_band_layout(const Geom& g, int He)
     const size_t cells = w1 * g.H * g.D;
     l.inL = take((size_t)g.W * He);
     l.inR = take((size_t)g.W * He);
-    l.cL = take((size_t)g.W * He * 8);
-    l.cR = take((size_t)g.W * He * 8);
+    auto take_codes = [&](size_t n) { return take((n + 2 * sgm::kCodeMargin) * 8) + 8 * sgm::kCodeMargin; };
+    l.cL = take_codes((size_t)g.W * He);
+    l.cR = take_codes((size_t)g.W * He);
     l.vol_bytes = align_up(cells + kTrashBytes);
     l.vols = take(l.vol_bytes * 8);
     const unsigned masks[3] = {kDirsHoriz, kDirsDown, kDirsUp};

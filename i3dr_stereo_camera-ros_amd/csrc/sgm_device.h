@@ -21,6 +21,9 @@ __host__ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
+// Readable codes kept before and after every census code image in the workspace: the row
+// sweeps' segment loads run unclamped past the row ends (census_sgm.hip seg_load_u).
+constexpr int kCodeMargin = 1024;
 constexpr int kInf = 0x3FFF;  // > any u8 path cost and any census S (<= 8*255)
 
 // Geometry + effective parameters of one match (computed on the host, passed by value).

@@ -47,6 +47,10 @@ CASES = [
     dict(num_disparities=512),
     dict(num_disparities=64, p2=250),         # clamped to 193 (u8 path costs)
     dict(num_disparities=400, min_disparity=3),   # D % 32 == 16: a lane straddles D (DPL 32)
+    dict(num_disparities=64, uniqueness_ratio=99),
+    dict(num_disparities=64, uniqueness_ratio=100),   # every d qualifies when minS > 0
+    dict(num_disparities=48, uniqueness_ratio=130),   # > 100: S > 0 qualifies when minS == 0
+    dict(num_disparities=32, uniqueness_ratio=1, p2=15),
 ]
 
 

@@ -1,0 +1,17 @@
+#!/bin/bash
+# env_variants.sh "ENV=.. ENV2=.." ... — C3 bench of the in-tree build under each environment
+set -u
+mkdir -p gpurun_out
+: > gpurun_out/env_variants.txt
+i=0
+for e in "" "$@"; do
+  i=$((i+1))
+  env $e timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/e_$i.log 2>&1 || { echo "[$e] failed"; tail -5 gpurun_out/e_$i.log; exit 1; }
+  python - "$e" gpurun_out/e_$i.log >> gpurun_out/env_variants.txt <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[2]) if l.startswith('{')][-1])
+st = ' '.join(f"{s['name']}={s['avg_ms']:.3f}" for s in d['stages'])
+print(f"[{sys.argv[1]:>24}] {d['value']:8.1f} pairs/s  {st}")
+PY
+done
+cat gpurun_out/env_variants.txt
