@@ -97,6 +97,25 @@ __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 
     }
 }
 
+// the same from a raw buffer (base wave-uniform, byte offset off per lane)
+template <int DPL>
+__device__ __forceinline__ void wload_buf(const uint8_t* base, uint32_t off, uint32_t (&wd)[(DPL + 3) / 4])
+{
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
+    if constexpr (DPL == 2) { wd[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0); }
+    else if constexpr (DPL == 4) { wd[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0); }
+    else if constexpr (DPL == 8) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        wd[0] = v[0]; wd[1] = v[1];
+    } else {
+#pragma unroll
+        for (int q = 0; q < DPL / 16; q++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * q, 0, 0);
+            wd[4 * q] = v[0]; wd[4 * q + 1] = v[1]; wd[4 * q + 2] = v[2]; wd[4 * q + 3] = v[3];
+        }
+    }
+}
+
 // dst_hi: where bytes 16..31 go when DPL == 32 (D not a multiple of 32 leaves the lane that
 // straddles D half valid: its upper half must go to the trash slot, not the next pixel)
 template <int DPL>
@@ -623,7 +642,8 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
     uint32_t* sl = lds;                           // 4 waves x 4 rows x 16 lanes x 2*NWD packed S dwords
     RowLds R(lds, (char*)lds + wta_key_bytes<DPL>(g.W), g.W);   // R.key aliases sl
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave index (uniform: SGPR)
     const int r = lane >> 4, p = lane & 15;
     R.init(g, tid, kWG, false);
     const bool lane_act = EXACT || p * DPL < g.D;
@@ -645,10 +665,16 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     const float inv_u = 1.0f / (float)max(100 - g.uniq, 1);
     const int n = g.width1;
     const int nq = (n + 3) / 4;
+    // pixel 4q + r: the group's base is wave-uniform, the lane keeps one offset. The last
+    // group reads up to 3 pixels past the row (the next row, or the volume's trash slot
+    // after the last row); their results are never stored.
+    // Buffer loads (one descriptor per volume from the wave-uniform group base, the lane's
+    // offset in a VGPR): no per-lane 64-bit address arithmetic.
+    const uint32_t loff = off0 + (uint32_t)(r * g.D);
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
-        const uint32_t off = off0 + (uint32_t)(min(4 * q + r, n - 1) * g.D);
+        const uint8_t* rowq = vols + row0 + (size_t)(4 * q) * g.D;
 #pragma unroll
-        for (int vv = 0; vv < 8; vv++) wload<DPL>(vols + (size_t)vv * vol_bytes + row0 + off, v[vv]);
+        for (int vv = 0; vv < 8; vv++) wload_buf<DPL>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
     };
     // S in u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]); halves past D or past
     // the lane's DPL are 0xFFFF. The next pixel group's loads are summed at the end of an
