@@ -14,11 +14,8 @@
 #ifndef SGM_WPE
 #define SGM_WPE 4          // minimum waves per SIMD of the path kernels (register budget)
 #endif
-#ifndef SGM_SEG_UNCLAMPED
-#define SGM_SEG_UNCLAMPED 1
-#endif
-#ifndef SGM_ROWS_PRELOAD
-#define SGM_ROWS_PRELOAD 0
+#ifndef SGM_ROWS_LPL8
+#define SGM_ROWS_LPL8 0    // 1: row sweeps with 8 lanes per path line for D <= 256 (RowsCfg; measured slower)
 #endif
 
 #include <algorithm>
@@ -200,15 +197,16 @@ __device__ __forceinline__ int tdiv_rcp(int num, int den)
     return q;
 }
 
-// Relative state of a line from its absolute costs: Lr = Labs - min over the row's D
-template <int DPL>
+// Relative state of a line from its absolute costs: Lr = Labs - min over the line's D
+// (LPL lanes per line: 16 = a whole 16-lane row, 8 = one parity of a row, see p16_rows)
+template <int DPL, int LPL = 16>
 __device__ __forceinline__ void p16_relative(const uint32_t (&Labs)[DPL / 2], uint32_t (&Lr)[DPL / 2])
 {
     constexpr int M = DPL / 2;
     uint32_t mn = Labs[0];
 #pragma unroll
     for (int i = 1; i < M; i += 2) mn = (i + 1 < M) ? pk_min3_p(mn, Labs[i], Labs[i + 1]) : pk_min(mn, Labs[i]);
-    mn = row_min_u32(pk_min(mn, alignbit16(mn, mn)));     // (min, min) in every lane of the row
+    mn = line_min_u32<LPL>(pk_min(mn, alignbit16(mn, mn)));   // (min, min) in every lane of the line
     const uint32_t off = mn - kBaseP2;                    // pattern(L) - off = pattern(L - min)
 #pragma unroll
     for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], off);
@@ -220,16 +218,19 @@ __device__ __forceinline__ void p16_relative(const uint32_t (&Labs)[DPL / 2], ui
 // Per pair: q = Lr + P1 (1), neighbour align (1), minimum3 (1), min P2 (1), 4 xor + 4 bcnt
 // + 1 shift-add for the two costs (the low cost rides on v_bcnt's accumulator), 1/2 for the
 // min reduction, 1 subtract.
-template <int DPL, bool EXACT, typename F>
+// LPL = 8: the line's lanes are every other lane of a 16-lane row, so the neighbouring lane
+// of the same line is 2 lanes away (row_shr:2 / row_shl:2; both lines' edge lanes read kInf).
+template <int DPL, bool EXACT, int LPL = 16, typename F>
 __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F crk, uint32_t P1P1, uint32_t P2P2,
                                          const uint32_t (&imask)[DPL / 2], uint32_t (&Labs)[DPL / 2])
 {
     constexpr int M = DPL / 2;
+    constexpr int SH = LPL == 16 ? 1 : 2;
     uint32_t q[M];
 #pragma unroll
     for (int i = 0; i < M; i++) q[i] = pk_add(Lr[i], P1P1);
-    const uint32_t X = row_shr1(q[M - 1], kInfP2);        // previous lane: its .hi is q(d0 - 1)
-    const uint32_t Y = row_shl1(q[0], kInfP2);            // next lane: its .lo is q(d0 + DPL)
+    const uint32_t X = row_shr_n<SH>(q[M - 1], kInfP2);   // previous lane: its .hi is q(d0 - 1)
+    const uint32_t Y = row_shl_n<SH>(q[0], kInfP2);       // next lane: its .lo is q(d0 + DPL)
     uint32_t Oprev = alignbit16(q[0], X);                 // (q(d-1), q(d)) for pair 0
 #pragma unroll
     for (int i = 0; i < M; i++) {
@@ -241,7 +242,7 @@ __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F
         Labs[i] = L;
         Oprev = Onext;
     }
-    p16_relative<DPL>(Labs, Lr);
+    p16_relative<DPL, LPL>(Labs, Lr);
 }
 
 // imask: kInfP in the halves with d >= D (0 elsewhere); start: the relative state of a
@@ -283,7 +284,6 @@ __device__ __forceinline__ T pick4(const T (&a)[kMaxGroup], int f)
 
 constexpr int kWG = 256;          // 4 waves
 constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
-constexpr int kColsPerWG = 16;    // row sweeps: 4 columns per wave
 
 // ---------------------------------------------------------------- horizontal scans ----
 // Scalar operands per step come from 16-step chunks held one value per lane (lane j of a
@@ -365,95 +365,93 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
 }
 
 // ---------------------------------------------------------------- row sweeps ----------
-// Workgroup = 4 waves = 16 adjacent lines; slot j = 4*wave + row. Each step the WG stages
-// the row's right-code segment (16*DPL + 15 codes) and the 16 left codes in LDS, double-
-// buffered, one barrier per step; the segment is padded by one code per 16 so the lanes'
-// strided window reads spread over the banks.
-template <int DPL>
+// Workgroup = 4 waves of 64 / LPL lines each (NL = 256 / LPL adjacent lines). LPL = 16: a
+// line is one 16-lane row (slot j = 4*wave + row). LPL = 8: a 16-lane row holds two lines,
+// interleaved by lane parity (lane = 2*p + line), so a line's d-neighbour lanes are 2 apart
+// and its min over D stays inside the parity (p16_step, line_min_u32); slot j =
+// 8*wave + 2*row + parity. Each step the WG stages the row's right-code segment
+// (LPL*DPL + NL - 1 codes) and the NL left codes in LDS, double-buffered, one barrier per
+// step. The segment is padded so that the lanes' strided window reads spread over the
+// banks (LPL 16: one code per 16, a lane stride of 17 codes; LPL 8: four codes per 32, a
+// lane stride of 36 codes = 8 banks, conflict-free for the four lines of a 32-lane half).
+template <int DPL, int LPL>
 struct RowSeg {
-    static constexpr int NSEG = 16 * DPL + 15;
-    static constexpr int NPAD = NSEG + NSEG / 16 + 1;        // padded cR part
-    static constexpr int NTOT = NSEG + 16;                   // codes staged per step
+    static constexpr int NL = kWG / LPL;                     // lines per workgroup
+    static constexpr int NSEG = LPL * DPL + NL - 1;
+    static constexpr int NPAD = LPL == 16 ? NSEG + NSEG / 16 + 1 : NSEG + 4 * (NSEG / 32) + 4;
+    static constexpr int NTOT = NSEG + NL;                   // codes staged per step
     static constexpr int NLOAD = (NTOT + kWG - 1) / kWG;     // per thread
-    static constexpr int BUF = NPAD + 16 + kWG;              // + cL + dummy slots
-    static __device__ __forceinline__ int phys(int e) { return e + (e >> 4); }
+    static constexpr int BUF = NPAD + NL + kWG;              // + cL + dummy slots
+    static __device__ __forceinline__ int phys(int e) { return LPL == 16 ? e + (e >> 4) : e + 4 * (e >> 5); }
+};
+// row-sweep geometry for a 16-lane DPL: D <= 256 sweeps with 8 lanes per line (twice the
+// disparities per lane: the per-step overhead and the row's code reads are shared by 32
+// lines), D = 512 keeps 16 lanes (a 32-disparity lane already)
+template <int DPL16>
+struct RowsCfg {
+#if SGM_ROWS_LPL8
+    static constexpr int LPL = DPL16 <= 16 ? 8 : 16;
+#else
+    static constexpr int LPL = 16;
+#endif
+    static constexpr int DPL = DPL16 * 16 / LPL;
+    static constexpr int NL = kWG / LPL;
 };
 
-template <int DPL>
-__device__ __forceinline__ void seg_load(uint64_t (&v)[RowSeg<DPL>::NLOAD], const uint64_t* cL, const uint64_t* cR,
-                                         const Geom& g, int rx, int ry, int xb, int s, int tid)
-{
-    using RS = RowSeg<DPL>;
-    const int y = ry > 0 ? s : g.H - 1 - s;
-    const int yc = min(max(y, 0), g.H - 1);
-    // one wave-uniform base for both code images + 32-bit element offsets
-    // (SGPR-base + VGPR-offset loads instead of per-lane 64-bit address arithmetic)
-    const uint64_t* base = cL < cR ? cL : cR;
-    const uint32_t oL = (uint32_t)(cL - base) + (uint32_t)(yc * g.W);
-    const uint32_t oR = (uint32_t)(cR - base) + (uint32_t)(yc * g.W);
-    const int xs = xb + rx * s;
-    const int seg0 = xs - g.minD - 16 * DPL + 1;
-#pragma unroll
-    for (int m = 0; m < RS::NLOAD; m++) {
-        const int q = min(tid + m * kWG, RS::NTOT - 1);
-        const int idx = q < RS::NSEG ? seg0 + q : xs + (q - RS::NSEG);
-        v[m] = base[(q < RS::NSEG ? oR : oL) + (uint32_t)min(max(idx, 0), g.W - 1)];
-    }
-}
-
-// Unclamped form: the code images have kCodeMargin readable codes before and after them
-// (workspace layout), and the codes outside [0, W) of a row feed only lines or lanes whose
-// results go to the trash slot, so each lane keeps ONE byte offset for the whole sweep and a
-// step moves the wave-uniform base (SGPR base + VGPR offset loads, no per-step VALU).
-template <int DPL>
+// The code images have kCodeMargin readable codes before and after them (workspace
+// layout), and the codes outside [0, W) of a row feed only lines or lanes whose results go
+// to the trash slot, so each lane keeps ONE byte offset for the whole sweep and a step moves
+// the wave-uniform base (SGPR base + VGPR offset loads, no per-step VALU).
+template <int DPL, int LPL>
+using SegRegs = uint64_t[RowSeg<DPL, LPL>::NLOAD];     // one step's staged codes per thread
+template <int DPL, int LPL>
 struct SegAddr {
-    uint32_t off[RowSeg<DPL>::NLOAD];   // byte offsets from the step base
-    const char* lo;                     // min(cL, cR) - bias codes
-    int bias;
+    uint32_t off[RowSeg<DPL, LPL>::NLOAD];   // byte offsets from the step base
+    const char* lo;                          // min(cL, cR) - bias codes
 };
-template <int DPL>
-__device__ __forceinline__ SegAddr<DPL> seg_addr(const uint64_t* cL, const uint64_t* cR, const Geom& g, int tid)
+template <int DPL, int LPL>
+__device__ __forceinline__ SegAddr<DPL, LPL> seg_addr(const uint64_t* cL, const uint64_t* cR, const Geom& g, int tid)
 {
-    using RS = RowSeg<DPL>;
-    SegAddr<DPL> a;
+    using RS = RowSeg<DPL, LPL>;
+    SegAddr<DPL, LPL> a;
     const uint64_t* base = cL < cR ? cL : cR;
-    a.bias = 16 * DPL + max(g.minD, 0);                 // makes every lane offset >= 0
-    a.lo = (const char*)base - (size_t)8 * a.bias;
+    const int bias = LPL * DPL + max(g.minD, 0);        // makes every lane offset >= 0
+    a.lo = (const char*)base - (size_t)8 * bias;
 #pragma unroll
     for (int m = 0; m < RS::NLOAD; m++) {
         const int q = min(tid + m * kWG, RS::NTOT - 1);
-        const int rel = q < RS::NSEG ? (int)(cR - base) + q - g.minD - 16 * DPL + 1 : (int)(cL - base) + (q - RS::NSEG);
-        a.off[m] = (uint32_t)(8 * (rel + a.bias));
+        const int rel = q < RS::NSEG ? (int)(cR - base) + q - g.minD - LPL * DPL + 1 : (int)(cL - base) + (q - RS::NSEG);
+        a.off[m] = (uint32_t)(8 * (rel + bias));
     }
     return a;
 }
-template <int DPL>
-__device__ __forceinline__ void seg_load_u(uint64_t (&v)[RowSeg<DPL>::NLOAD], const SegAddr<DPL>& a, const Geom& g,
-                                           int rx, int ry, int xb, int s)
+template <int DPL, int LPL>
+__device__ __forceinline__ void seg_load(SegRegs<DPL, LPL>& v, const SegAddr<DPL, LPL>& a,
+                                         const Geom& g, int rx, int ry, int xb, int s)
 {
     const int y = ry > 0 ? s : g.H - 1 - s;
     const int yc = min(max(y, 0), g.H - 1);
     const char* sb = a.lo + (size_t)8 * ((size_t)yc * g.W + (xb + rx * s));   // wave-uniform
 #pragma unroll
-    for (int m = 0; m < RowSeg<DPL>::NLOAD; m++) v[m] = *(const uint64_t*)(sb + a.off[m]);
+    for (int m = 0; m < RowSeg<DPL, LPL>::NLOAD; m++) v[m] = *(const uint64_t*)(sb + a.off[m]);
 }
 
-template <int DPL>
-__device__ __forceinline__ void seg_store(uint64_t* buf, const uint64_t (&v)[RowSeg<DPL>::NLOAD], int tid)
+template <int DPL, int LPL>
+__device__ __forceinline__ void seg_store(uint64_t* buf, const SegRegs<DPL, LPL>& v, int tid)
 {
-    using RS = RowSeg<DPL>;
+    using RS = RowSeg<DPL, LPL>;
 #pragma unroll
     for (int m = 0; m < RS::NLOAD; m++) {
         const int q0 = tid + m * kWG;
-        const int at = q0 < RS::NSEG ? RS::phys(q0) : (q0 < RS::NTOT ? RS::NPAD + (q0 - RS::NSEG) : RS::NPAD + 16 + tid);
+        const int at = q0 < RS::NSEG ? RS::phys(q0) : (q0 < RS::NTOT ? RS::NPAD + (q0 - RS::NSEG) : RS::NPAD + RS::NL + tid);
         buf[at] = v[m];
     }
 }
 
 // Relative state of a line continued from a neighbouring band: the u8 costs Lprev stored
 // for its predecessor pixel (src: the lane's DPL bytes) -> Lprev - min Lprev. Every lane of
-// the row takes part (row-wide min); the caller selects per line.
-template <int DPL, bool EXACT>
+// the line takes part (line-wide min); the caller selects per line.
+template <int DPL, bool EXACT, int LPL>
 __device__ __forceinline__ void p16_seed(const uint8_t* src, const uint32_t (&imask)[DPL / 2], uint32_t (&Lr)[DPL / 2])
 {
     uint32_t wd[(DPL + 3) / 4], Labs[DPL / 2];
@@ -464,25 +462,29 @@ __device__ __forceinline__ void p16_seed(const uint8_t* src, const uint32_t (&im
         Labs[i] = pr | kBaseP2;                           // bytes -> biased-f16 patterns
         if (!EXACT) Labs[i] = pk_max(Labs[i], imask[i]);
     }
-    p16_relative<DPL>(Labs, Lr);
+    p16_relative<DPL, LPL>(Labs, Lr);
 }
 
-template <int DPL, bool EXACT>
+// NL lines of direction dir starting at base column xb (DPL disparities per lane, LPL
+// lanes per line; lds: 2 * RowSeg<DPL, LPL>::BUF codes).
+template <int DPL, bool EXACT, int LPL>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
                                          int xb, const PathLaunch16& pl, uint64_t* lds)
 {
-    using RS = RowSeg<DPL>;
+    using RS = RowSeg<DPL, LPL>;
     constexpr int M = DPL / 2;
+    constexpr int NL = RS::NL;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
-    const int r = lane >> 4, p = lane & 15;
-    const int j = 4 * w + r;                       // slot (line) of this row of lanes
+    const int r = lane >> 4;
+    const int p = LPL == 16 ? lane & 15 : (lane & 15) >> 1;            // lane within the line
+    const int j = LPL == 16 ? 4 * w + r : 8 * w + 2 * r + (lane & 1);  // slot (line) of the lane
     const int rx = dir_rx(dir), ry = dir_ry(dir);
     int s0, s1;
     if (rx == 0) { s0 = 0; s1 = g.H; }
-    else if (rx > 0) { s0 = max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = min(g.H, g.maxX1 - xb); }
-    else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + kColsPerWG - g.minX1); }
+    else if (rx > 0) { s0 = max(0, g.minX1 - xb - (NL - 1)); s1 = min(g.H, g.maxX1 - xb); }
+    else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + NL - g.minX1); }
     if (s0 >= s1) return;                          // uniform over the workgroup
     uint32_t imask[M], start[M];
     make_imask<DPL, EXACT>(p, g.D, imask, start);
@@ -497,7 +499,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         const bool cont = x >= g.minX1 && x < g.maxX1 && xp >= g.minX1 && xp < g.maxX1;
         const int xs = min(max(xp, g.minX1), g.maxX1 - 1) - g.minX1;
         uint32_t Ls[M];
-        p16_seed<DPL, EXACT>(bnd + bnd_slot_of(dir) * pl.bnd_slot + (size_t)xs * g.D + p * DPL, imask, Ls);
+        p16_seed<DPL, EXACT, LPL>(bnd + bnd_slot_of(dir) * pl.bnd_slot + (size_t)xs * g.D + p * DPL, imask, Ls);
 #pragma unroll
         for (int i = 0; i < M; i++) Lr[i] = cont ? Ls[i] : Lr[i];
         pv = cont;
@@ -507,7 +509,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     // stores: the step's row base is wave-uniform (64-bit, scalar math); lanes add a 32-bit
     // offset inside the row (< width1 * D), or go to their trash slot
     uint8_t* const tr = trash + (tid & 63) * DPL;
-    const int e_hi = j + (16 - p) * DPL - 1;       // segment index of the lane's k = 0 code
+    const int e_hi = j + (LPL - p) * DPL - 1;      // segment index of the lane's k = 0 code
 
     // Segments are staged in LDS (double buffer, one barrier per step) from registers loaded
     // 3 steps ahead: the counted vmcnt wait for a segment then leaves the stores of the last
@@ -515,17 +517,12 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     uint64_t* buf0 = lds;
     uint64_t* buf1 = lds + RS::BUF;
     uint64_t R0[RS::NLOAD], R1[RS::NLOAD], R2[RS::NLOAD], R3[RS::NLOAD];
-#if SGM_SEG_UNCLAMPED
-    const SegAddr<DPL> sa = seg_addr<DPL>(cL, cR, g, tid);
-#define SEG_LOAD(R, st) seg_load_u<DPL>(R, sa, g, rx, ry, xb, st)
-#else
-#define SEG_LOAD(R, st) seg_load<DPL>(R, cL, cR, g, rx, ry, xb, st, tid)
-#endif
-    SEG_LOAD(R0, s0);
-    seg_store<DPL>(buf0, R0, tid);
-    SEG_LOAD(R1, min(s0 + 1, s1 - 1));
-    SEG_LOAD(R2, min(s0 + 2, s1 - 1));
-    SEG_LOAD(R3, min(s0 + 3, s1 - 1));
+    const SegAddr<DPL, LPL> sa = seg_addr<DPL, LPL>(cL, cR, g, tid);
+    seg_load<DPL, LPL>(R0, sa, g, rx, ry, xb, s0);
+    seg_store<DPL, LPL>(buf0, R0, tid);
+    seg_load<DPL, LPL>(R1, sa, g, rx, ry, xb, min(s0 + 1, s1 - 1));
+    seg_load<DPL, LPL>(R2, sa, g, rx, ry, xb, min(s0 + 2, s1 - 1));
+    seg_load<DPL, LPL>(R3, sa, g, rx, ry, xb, min(s0 + 3, s1 - 1));
     __syncthreads();
 
     auto step = [&](int s, const uint64_t* bufc) {
@@ -537,15 +534,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         // path start (first valid pixel of the line): L = C. The P2 cap of the recurrence is
         // lowered to "0" (kBase), which clamps every candidate: one select per step.
         const uint32_t P2x = pv ? P2P2 : kBaseP2;
-#if SGM_ROWS_PRELOAD
-        uint64_t crv[DPL];
-#pragma unroll
-        for (int k = 0; k < DPL; k++) crv[k] = bufc[RS::phys(e_hi - k)];
-        __builtin_amdgcn_sched_barrier(0);
-        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return crv[k]; }, P1P1, P2x, imask, Labs);
-#else
-        p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
-#endif
+        p16_step<DPL, EXACT, LPL>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
         const bool ok = valid && lane_act;
         uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
         uint8_t* const dst = ok ? vrow + (uint32_t)((x - g.minX1) * g.D + p * DPL) : tr;
@@ -556,9 +545,9 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     // (s + 1) % 4) goes to buf[(s + 1) & 1] and set s % 4 is reloaded with segment s + 4
     auto body = [&](int s, const uint64_t* bcur, uint64_t* bnext, uint64_t (&Rnext)[RS::NLOAD],
                     uint64_t (&Rfree)[RS::NLOAD]) {
-        SEG_LOAD(Rfree, min(s + 4, s1 - 1));
+        seg_load<DPL, LPL>(Rfree, sa, g, rx, ry, xb, min(s + 4, s1 - 1));
         step(s, bcur);
-        seg_store<DPL>(bnext, Rnext, tid);
+        seg_store<DPL, LPL>(bnext, Rnext, tid);
         __syncthreads();
     };
     for (int s = s0; s < s1; s += 4) {
@@ -567,14 +556,18 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         body(s + 2, buf0, buf1, R3, R2);
         body(s + 3, buf1, buf0, R0, R3);
     }
-#undef SEG_LOAD
 }
 
-// One work-list entry: 16 lines of one direction of one frame (lds: 2 * RowSeg<DPL>::BUF).
+// One work-list entry: the lines of one block of one direction of one frame (16 rows for
+// the horizontal scans, RowsCfg<DPL>::NL columns for the row sweeps; lds: rows_lds_codes).
+template <int DPL>
+__host__ __device__ constexpr int rows_lds_codes() { return 2 * RowSeg<RowsCfg<DPL>::DPL, RowsCfg<DPL>::LPL>::BUF; }
+
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_bytes, size_t trash_off,
                                               const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
+    using RC = RowsCfg<DPL>;
     const int dir = (int)(it >> 24);
     const int f = (int)((it >> 22) & 3u);
     const int lb = (int)(it & 0x3FFFFFu);
@@ -585,7 +578,7 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     uint8_t* trash = V + trash_off;
     if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
     else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-    else p16_rows<DPL, EXACT>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * kColsPerWG, pl, lds);
+    else p16_rows<RC::DPL, EXACT, RC::LPL>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
 }
 
 // SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
@@ -604,7 +597,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ?
 void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
                       const uint32_t* __restrict__ items, uint64_t* __restrict__ trace)
 {
-    __shared__ uint64_t lds[2 * RowSeg<DPL>::BUF];
+    __shared__ uint64_t lds[rows_lds_codes<DPL>()];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
     if (trace && (threadIdx.x & 63) == 0)        // debug timeline (SGM_TRACE): one record per wave
@@ -897,6 +890,17 @@ hipError_t launch_census(const uint8_t* L, const uint8_t* R, size_t stride, int 
 }
 
 static int dpl16_for(int D) { return D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
+// lines per row-sweep workgroup (RowsCfg<DPL>::NL of the launch's DPL)
+static int rows_lines(int D)
+{
+    switch (dpl16_for(D)) {
+    case 2: return RowsCfg<2>::NL;
+    case 4: return RowsCfg<4>::NL;
+    case 8: return RowsCfg<8>::NL;
+    case 16: return RowsCfg<16>::NL;
+    default: return RowsCfg<32>::NL;
+    }
+}
 
 PathLaunch16 make_path_launch16(const Geom& g)
 {
@@ -927,13 +931,14 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
         }
         const int rx = dir_rx(dir);
         const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
-        const int nb = (hi - pl.xb_lo[dir] + kColsPerWG - 1) / kColsPerWG;
+        const int NL = rows_lines(g.D);
+        const int nb = (hi - pl.xb_lo[dir] + NL - 1) / NL;
         for (int b = 0; b < nb; b++) {
-            const int xb = pl.xb_lo[dir] + b * kColsPerWG;
+            const int xb = pl.xb_lo[dir] + b * NL;
             int s0, s1;      // same step range as p16_rows
             if (rx == 0) { s0 = 0; s1 = g.H; }
-            else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (kColsPerWG - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
-            else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + kColsPerWG - g.minX1); }
+            else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (NL - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
+            else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + NL - g.minX1); }
             for (int f = 0; f < group; f++) v.push_back({std::max(s1 - s0, 0), path_item(dir, b, f)});
         }
     }
@@ -1053,7 +1058,7 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
 {
     const int n_census = ((g.W + 63) / 64) * ((g.H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
     dim3 grid(n_items + g.H * wf.n + n_census), block(kWG);
-    const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * 2 * RowSeg<DPL>::BUF,
+    const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * rows_lds_codes<DPL>(),
                                  (size_t)(kCensusRows + 6) * 72});
     uint64_t* tr = trace_buffer((int)grid.x);
     // WTA rows interleaved one per 2.75 blocks (C3 sweep: after the paths 554 pairs/s, 1/2 498,

@@ -343,6 +343,27 @@ __device__ __forceinline__ uint64_t row_shr1_u64(uint64_t v, uint64_t old) {
 __device__ __forceinline__ uint64_t row_shl1_u64(uint64_t v, uint64_t old) {
     return ((uint64_t)row_shl1((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) | row_shl1((uint32_t)v, (uint32_t)old);
 }
+// shift by N lanes inside 16-lane rows (lanes whose source is outside the row read `old`)
+template <int N>
+__device__ __forceinline__ uint32_t row_shr_n(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x110 + N, 0xf, 0xf, false);
+}
+template <int N>
+__device__ __forceinline__ uint32_t row_shl_n(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x100 + N, 0xf, 0xf, false);
+}
+// unsigned min over the lanes of one path line, result in every lane of the line:
+// LPL = 16: the whole 16-lane row; LPL = 8: the lanes of one parity in the row (two
+// interleaved lines per row, lane = 2 * p + line)
+template <int LPL>
+__device__ __forceinline__ uint32_t line_min_u32(uint32_t v) {
+    if constexpr (LPL == 16)
+        v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));       // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, true));      // row_ror:4
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, true));      // row_ror:8
+    return v;
+}
 // unsigned min over the 16 lanes of each row, result in every lane of the row
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
     v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));    // quad_perm [1,0,3,2]
