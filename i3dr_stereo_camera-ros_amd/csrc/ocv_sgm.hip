@@ -3,9 +3,10 @@
 // Bit-exact with the CPU restatement oracle/sgm_oracle.c `ocv_match` (which follows
 // OpenCV's sequential raster loop); here every stage is re-expressed in parallel form:
 //   k_ocv_prefilter  Sobel-x prefilter + raw channel, columns 0 / W-1 forced to ftzero
-//   k_ocv_pixcost    Birchfield-Tomasi cost of both channels (raw >> 2), int16 [H][w1][D]
-//   k_ocv_hsum       horizontal SAD box, replicate clamp to [0, width1)        (exact)
-//   k_ocv_vsum       vertical box + P2 offset + OpenCV's bottom-row quirk:
+//   k_ocv_pixhsum    Birchfield-Tomasi cost of both channels (raw >> 2) and the horizontal
+//                    SAD box (replicate clamp to [0, width1)) in one pass through LDS;
+//                    k_ocv_pixcost + k_ocv_hsum unfused when the LDS tile would not fit
+//   k_ocv_vsum_seg   vertical box + P2 offset + OpenCV's bottom-row quirk:
 //                    rows with y + SH2 >= H are never recomputed (MODE_SGBM keeps the
 //                    last computed row, MODE_HH keeps the P2 initialisation)
 //   k_ocv_paths      each direction independently (L depends only on its own path);
@@ -90,28 +91,95 @@ __global__ __launch_bounds__(256) void k_ocv_hsum(const int16_t* __restrict__ pi
     }
 }
 
-// thread per (x1, d): running vertical box along y, C' = P2 + SAD with the bottom-row rule
-__global__ __launch_bounds__(256) void k_ocv_vsum(const int16_t* __restrict__ hs, Geom g, int fullDP,
-                                                  int16_t* __restrict__ C)
+// Pixel cost + horizontal SAD box fused: one block per XB output pixels of a row. The BT
+// intervals of both images and the pixel costs of the XB + 2*SW2 columns the box reads
+// (positions clamped to [0, width1), as the running sum's replicate rule) live in LDS; the
+// box is a direct (2*SW2+1)-term sum of them — the same integer as the running sum.
+constexpr int kPixXB = 32;
+__global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__ planes, Geom g,
+                                                     int16_t* __restrict__ hs)
+{
+    extern __shared__ uint8_t lds_pix[];
+    const int y = blockIdx.y, x0 = blockIdx.x * kPixXB, tid = threadIdx.x;
+    const int SW2 = g.SW2, NX = kPixXB + 2 * SW2;          // pixel-cost columns staged
+    const int NR = NX + g.D - 1;                           // right-image BT entries needed
+    const size_t plane = (size_t)g.W * g.H;
+    int16_t* P = (int16_t*)lds_pix;                        // [NX][D]
+    uint8_t* bl = lds_pix + (size_t)2 * NX * g.D;          // left  (u, lo, hi) x 2 channels x NX
+    uint8_t* br = bl + 6 * NX;                             // right (v, lo, hi) x 2 channels x NR
+    // staged column i -> x1 = clamp(x0 - SW2 + i); right entry r -> xr = xlo - minD - (D-1) + r
+    const int xlo = g.minX1 + min(max(x0 - SW2, 0), g.width1 - 1);
+    for (int i = tid; i < 2 * NX; i += 256) {
+        const int c = i / NX, k = i - c * NX;
+        const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
+        int u, lo, hi;
+        bt_lohi(planes + c * plane + (size_t)y * g.W, x, g.W, u, lo, hi);
+        bl[(c * 3 + 0) * NX + k] = (uint8_t)u; bl[(c * 3 + 1) * NX + k] = (uint8_t)lo; bl[(c * 3 + 2) * NX + k] = (uint8_t)hi;
+    }
+    const int xr0 = xlo - g.minD - (g.D - 1);
+    for (int i = tid; i < 2 * NR; i += 256) {
+        const int c = i / NR, r = i - c * NR;
+        const int xr = min(max(xr0 + r, 0), g.W - 1);
+        int v, lo, hi;
+        bt_lohi(planes + (2 + c) * plane + (size_t)y * g.W, xr, g.W, v, lo, hi);
+        br[(c * 3 + 0) * NR + r] = (uint8_t)v; br[(c * 3 + 1) * NR + r] = (uint8_t)lo; br[(c * 3 + 2) * NR + r] = (uint8_t)hi;
+    }
+    __syncthreads();
+    for (int i = tid; i < NX * g.D; i += 256) {
+        const int k = i / g.D, d = i - k * g.D;
+        const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
+        const int r = x - g.minD - d - xr0;                // index of xr = x - minD - d
+        int acc = 0;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const int u = bl[(c * 3) * NX + k], ulo = bl[(c * 3 + 1) * NX + k], uhi = bl[(c * 3 + 2) * NX + k];
+            const int v = br[(c * 3) * NR + r], v0 = br[(c * 3 + 1) * NR + r], v1 = br[(c * 3 + 2) * NR + r];
+            const int c0 = max(0, max(u - v1, v0 - u));
+            const int c1 = max(0, max(v - uhi, ulo - v));
+            acc += min(c0, c1) >> (c == 0 ? 0 : 2);
+        }
+        P[i] = (int16_t)acc;
+    }
+    __syncthreads();
+    const int nout = min(kPixXB, g.width1 - x0);
+    for (int i = tid; i < nout * g.D; i += 256) {
+        const int xo = i / g.D, d = i - xo * g.D;
+        int sum = 0;
+        for (int k = 0; k <= 2 * SW2; k++) sum += P[(xo + k) * g.D + d];
+        hs[((size_t)y * g.width1 + x0 + xo) * g.D + d] = (int16_t)sum;
+    }
+}
+
+// Vertical box + P2 offset + the bottom-row rule, in segments of kVsumRows rows per thread
+// (each segment starts from its own window sum; rows y >= 1 with y + SH2 >= H repeat the
+// value of row max(H - SH2 - 1, 0) in MODE_SGBM, or are P2 in MODE_HH).
+constexpr int kVsumRows = 64;
+__global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict__ hs, Geom g, int fullDP,
+                                                      int16_t* __restrict__ C)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= g.width1 * g.D) return;
-    const size_t rowStride = (size_t)g.width1 * g.D;
+    const size_t rs = (size_t)g.width1 * g.D;
     const int H = g.H, SH2 = g.SH2;
-    int s = hs[i] * (SH2 + 1);
-    for (int k = 1; k <= SH2; k++) s += hs[(size_t)min(k, H - 1) * rowStride + i];
-    int last = g.P2 + s;
-    C[i] = (int16_t)last;
-    for (int y = 1; y < H; y++) {
+    const int y0 = blockIdx.y * kVsumRows, y1 = min(H, y0 + kVsumRows);
+    auto window = [&](int y) {
+        int s = 0;
+        for (int k = y - SH2; k <= y + SH2; k++) s += hs[(size_t)min(max(k, 0), H - 1) * rs + i];
+        return s;
+    };
+    const int ylast = max(H - SH2 - 1, 0);                 // last row whose window is recomputed
+    const bool tail = y1 - 1 >= 1 && y1 - 1 + SH2 >= H;    // the segment reaches the repeated rows
+    const int rep = fullDP ? g.P2 : g.P2 + (tail ? window(ylast) : 0);
+    int s = window(y0);
+    for (int y = y0; y < y1; y++) {
         int v;
-        if (y + SH2 < H) {
-            s += hs[(size_t)(y + SH2) * rowStride + i] - hs[(size_t)max(y - SH2 - 1, 0) * rowStride + i];
+        if (y == 0 || y + SH2 < H) {
+            if (y > y0) s += hs[(size_t)(y + SH2) * rs + i] - hs[(size_t)max(y - SH2 - 1, 0) * rs + i];
             v = g.P2 + s;
-            last = v;
         } else {
-            v = fullDP ? g.P2 : last;
+            v = rep;
         }
-        C[(size_t)y * rowStride + i] = (int16_t)v;
+        C[(size_t)y * rs + i] = (int16_t)v;
     }
 }
 
@@ -162,57 +230,64 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     bool pv = false;
 #pragma unroll
     for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
-    if (ry == 0) {
-        const int y = b;
-        for (int i = 0; i < g.width1; i++) {
-            const int x1 = rx > 0 ? i : g.width1 - 1 - i;
-            const size_t o = ((size_t)y * g.width1 + x1) * g.D;
-            int Cp[DPL], L[DPL];
-#pragma unroll
-            for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; Cp[k] = d < g.D ? C[o + d] : 0; }
-            const int lmin = ocv_step<DPL>(Cp, Lp, mLp, pv, lane, g, L);
-#pragma unroll
-            for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; if (d < g.D) V[o + d] = (int16_t)L[k]; }
-            mLp = (int)(int16_t)wave_min(lmin);           // minLr is CostType
-#pragma unroll
-            for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-            pv = true;
-        }
-        return;
+    // The line as (x1, y) at step i: horizontal (ry == 0) = row b; row sweeps start on the
+    // first row at column b (b < width1) or on the entry column at row offset b - width1 + 1
+    int x0, s0, n;
+    if (ry == 0) { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = b; n = g.width1; }
+    else {
+        if (b < g.width1) { x0 = b; s0 = 0; }
+        else { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = b - g.width1 + 1; }
+        n = g.H - s0;
+        if (rx > 0) n = min(n, g.width1 - x0);
+        if (rx < 0) n = min(n, x0 + 1);
     }
-    // line start: b < width1 -> starts on the first row at column b; else starts on the
-    // entry column (x1 = 0 for rx > 0, width1 - 1 for rx < 0) at row offset b - width1 + 1
-    int x1, s0;
-    if (b < g.width1) { x1 = b; s0 = 0; }
-    else { x1 = rx > 0 ? 0 : g.width1 - 1; s0 = b - g.width1 + 1; }
-    for (int s = s0; s < g.H; s++) {
-        if (x1 < 0 || x1 >= g.width1) break;
-        const int y = ry > 0 ? s : g.H - 1 - s;
-        const size_t o = ((size_t)y * g.width1 + x1) * g.D;
-        int Cp[DPL], L[DPL];
+    auto cell = [&](int i) -> size_t {           // cell offset of step i (clamped to the line)
+        i = min(i, n - 1);
+        const int y = ry == 0 ? s0 : (ry > 0 ? s0 + i : g.H - 1 - (s0 + i));
+        return ((size_t)y * g.width1 + (x0 + rx * i)) * g.D;
+    };
+    // C of the next PF steps in flight (one global-load latency per PF steps, not per step)
+    constexpr int PF = 4;
+    int Cb[PF][DPL];
+    auto load = [&](int (&c)[DPL], int i) {
+        const size_t o = cell(i);
 #pragma unroll
-        for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; Cp[k] = d < g.D ? C[o + d] : 0; }
-        const int lmin = ocv_step<DPL>(Cp, Lp, mLp, pv, lane, g, L);
+        for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; c[k] = d < g.D ? C[o + d] : 0; }
+    };
 #pragma unroll
-        for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; if (d < g.D) V[o + d] = (int16_t)L[k]; }
-        mLp = (int)(int16_t)wave_min(lmin);
+    for (int q = 0; q < PF; q++) load(Cb[q], q);
+    for (int i0 = 0; i0 < n; i0 += PF) {
 #pragma unroll
-        for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-        pv = true;
-        x1 += rx;
+        for (int q = 0; q < PF; q++) {
+            const int i = i0 + q;
+            if (i < n) {                          // wave-uniform
+                const size_t o = cell(i);
+                int L[DPL];
+                const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, lane, g, L);
+#pragma unroll
+                for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; if (d < g.D) V[o + d] = (int16_t)L[k]; }
+                mLp = (int)(int16_t)wave_min(lmin);   // minLr is CostType
+#pragma unroll
+                for (int k = 0; k < DPL; k++) Lp[k] = L[k];
+                pv = true;
+            }
+            load(Cb[q], i + PF);
+        }
     }
 }
 
-// one wave per row: S = saturate(sum L) then the shared batched WTA + row epilogue
+// one workgroup (4 waves) per row, each wave a group of 4 pixels in turn: S = saturate(sum L)
+// then the shared batched WTA + row epilogue
 template <int DPL>
-__global__ __launch_bounds__(64) void k_ocv_wta(const int16_t* __restrict__ vols, size_t vol_elems, int ndir, Geom g,
-                                                int16_t* __restrict__ out, size_t out_stride)
+__global__ __launch_bounds__(256) void k_ocv_wta(const int16_t* __restrict__ vols, size_t vol_elems, int ndir, Geom g,
+                                                 int16_t* __restrict__ out, size_t out_stride)
 {
     extern __shared__ uint32_t lds_ocv[];
     RowLds R(lds_ocv, g.W);
-    const int lane = threadIdx.x, y = blockIdx.x;
-    R.init(g, lane, 64);
-    for (int i0 = 0; i0 < g.width1; i0 += 4) {
+    const int tid = threadIdx.x, lane = tid & 63, y = blockIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    R.init(g, tid, 256);
+    for (int i0 = 4 * w; i0 < g.width1; i0 += 16) {
         int S[4][DPL], xs[4], nvalid = 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -234,7 +309,7 @@ __global__ __launch_bounds__(64) void k_ocv_wta(const int16_t* __restrict__ vols
         }
         wta_batch<DPL, 4>(S, lane, xs, nvalid, g, R.drow, R.bst, R.mins);
     }
-    row_finish(g, lane, 64, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+    row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
 // ------------------------------------------------------------------------------------
@@ -245,9 +320,17 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 {
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes);
-    hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
-    hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
-    hipLaunchKernelGGL(k_ocv_vsum, dim3((g.width1 * g.D + 255) / 256), dim3(256), 0, st, bufB, g, fullDP, bufA);
+    const int NX = kPixXB + 2 * g.SW2;
+    const size_t lds = (size_t)2 * NX * g.D + 6 * NX + 6 * (NX + g.D - 1);
+    if (lds <= 64 * 1024) {
+        hipLaunchKernelGGL(k_ocv_pixhsum, dim3((g.width1 + kPixXB - 1) / kPixXB, g.H), dim3(256), lds, st, planes, g,
+                           bufB);
+    } else {                // very wide boxes x wide ranges: the unfused pair (no LDS staging)
+        hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
+        hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
+    }
+    hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows), dim3(256),
+                       0, st, bufB, g, fullDP, bufA);
     return hipGetLastError();
 }
 
@@ -276,10 +359,10 @@ hipError_t launch_ocv_wta(const int16_t* vols, size_t vol_elems, int ndir, const
 {
     const size_t lds = RowLds::bytes(g.W);
     switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_ocv_wta<1>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    case 2: hipLaunchKernelGGL(k_ocv_wta<2>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    case 4: hipLaunchKernelGGL(k_ocv_wta<4>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    default: hipLaunchKernelGGL(k_ocv_wta<8>, dim3(g.H), dim3(64), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
+    case 1: hipLaunchKernelGGL(k_ocv_wta<1>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
+    case 2: hipLaunchKernelGGL(k_ocv_wta<2>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
+    case 4: hipLaunchKernelGGL(k_ocv_wta<4>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
+    default: hipLaunchKernelGGL(k_ocv_wta<8>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
     }
     return hipGetLastError();
 }

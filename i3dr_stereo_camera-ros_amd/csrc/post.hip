@@ -110,11 +110,29 @@ __global__ __launch_bounds__(256) void k_spk_union(const int16_t* __restrict__ d
     }
 }
 
-__global__ __launch_bounds__(256) void k_spk_count(int W, int H, const int* __restrict__ lab, int* __restrict__ cnt)
+// After the union phase (a kernel boundary away): every label points straight at its root.
+// Concurrent rewrites only ever replace a label by one of its ancestors, so the chains other
+// threads are walking stay valid.
+__global__ __launch_bounds__(256) void k_spk_flatten(int W, int H, int* __restrict__ lab)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H || lab[i] < 0) return;
-    atomicAdd(&cnt[uf_root(lab, i)], 1);
+    lab[i] = uf_root(lab, i);
+}
+
+// Component sizes: the lanes of a wave that share a root add once (one atomic per distinct
+// root per wave instead of one per pixel: a large region is otherwise a single hot counter).
+__global__ __launch_bounds__(256) void k_spk_count(int W, int H, const int* __restrict__ lab, int* __restrict__ cnt)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int root = i < W * H ? lab[i] : -1;
+    uint64_t todo = __ballot(root >= 0);
+    while (todo) {
+        const int leader = __builtin_amdgcn_readlane(root, __builtin_ctzll(todo));
+        const uint64_t same = __ballot(root == leader) & todo;
+        if ((threadIdx.x & 63) == __builtin_ctzll(same)) atomicAdd(&cnt[leader], __builtin_popcountll(same));
+        todo &= ~same;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_spk_apply(int16_t* __restrict__ d, size_t stride, int W, int H, int newVal,
@@ -123,8 +141,8 @@ __global__ __launch_bounds__(256) void k_spk_apply(int16_t* __restrict__ d, size
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
-    if (lab[i] < 0) return;
-    if (cnt[uf_root(lab, i)] <= maxSize) {
+    const int root = lab[i];
+    if (root >= 0 && cnt[root] <= maxSize) {
         const int y = i / W, x = i - y * W;
         d[(size_t)y * stride + x] = (int16_t)newVal;
     }
@@ -137,6 +155,7 @@ hipError_t launch_speckle(int16_t* d, size_t stride, int W, int H, int newVal, i
     dim3 grid((n + 255) / 256), block(256);
     hipLaunchKernelGGL(k_spk_init, grid, block, 0, st, d, stride, W, H, newVal, lab, cnt);
     hipLaunchKernelGGL(k_spk_union, grid, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
+    hipLaunchKernelGGL(k_spk_flatten, grid, block, 0, st, W, H, lab);
     hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, lab, cnt);
     hipLaunchKernelGGL(k_spk_apply, grid, block, 0, st, d, stride, W, H, newVal, maxSize, lab, cnt);
     return hipGetLastError();

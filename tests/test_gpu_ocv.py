@@ -15,7 +15,9 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("h,w,minD,D,block,cap", [(12, 50, 0, 16, 5, 31), (9, 45, 4, 16, 7, 15),
                                                   (4, 40, -3, 16, 9, 63), (17, 70, 2, 32, 3, 1),
-                                                  (40, 200, 9, 64, 15, 31), (30, 300, 0, 128, 11, 20)])
+                                                  (40, 200, 9, 64, 15, 31), (30, 300, 0, 128, 11, 20),
+                                                  (130, 333, 5, 48, 9, 31),       # 3 vsum row segments
+                                                  (70, 400, 0, 256, 101, 31)])    # LDS tile too big: unfused
 def test_ocv_cost_volume(engine, oracle, pkg, mode, h, w, minD, D, block, cap):
     rng = np.random.default_rng(h * w + mode)
     left = rng.integers(0, 256, (h, w), dtype=np.uint8)
