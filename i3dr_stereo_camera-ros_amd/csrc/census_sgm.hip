@@ -177,26 +177,6 @@ __device__ __forceinline__ uint32_t pk_shl(uint32_t a, int sh)
     return as_u(as_v2(a) << (u16x2_t){(unsigned short)sh, (unsigned short)sh});
 }
 __device__ __forceinline__ uint32_t pk_subs(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_sub_sat(as_v2(a), as_v2(b))); }
-// sum over the 16 lanes of each row, result in every lane of the row
-__device__ __forceinline__ uint32_t row_sum_u32(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true);    // quad_perm [1,0,3,2]
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true);    // quad_perm [2,3,0,1]
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, true);   // row_ror:4
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, true);   // row_ror:8
-    return v;
-}
-// C-style truncating num / den (|num| < 2^24, den > 0) from the hardware reciprocal: the
-// estimate is within one of the quotient, then fixed like tdiv()
-__device__ __forceinline__ int tdiv_rcp(int num, int den)
-{
-    int q = (int)__builtin_truncf((float)num * __builtin_amdgcn_rcpf((float)den));
-    const int r = num - q * den;
-    if (num >= 0) q += (r >= den) ? 1 : (r < 0 ? -1 : 0);
-    else          q += (r <= -den) ? -1 : (r > 0 ? 1 : 0);
-    return q;
-}
-
 // Relative state of a line from its absolute costs: Lr = Labs - min over the line's D
 // (LPL lanes per line: 16 = a whole 16-lane row, 8 = one parity of a row, see p16_rows)
 template <int DPL, int LPL = 16>

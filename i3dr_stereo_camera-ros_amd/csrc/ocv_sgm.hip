@@ -11,8 +11,9 @@
 //                    last computed row, MODE_HH keeps the P2 initialisation)
 //   k_ocv_paths      each direction independently (L depends only on its own path);
 //                    int16 storage of L and minL as OpenCV's CostType
-//   k_ocv_wta        S = saturate(sum of L) (all L >= 0 inside the parity domain, so the
-//                    saturating order is irrelevant) + the shared WTA / LR row code.
+//   k_ocv_wta16      S = saturate(sum of L) (all L >= 0 inside the parity domain, so the
+//                    saturating order is irrelevant), 16 lanes per pixel, + the shared
+//                    disp2 / LR row code.
 // Parity domain: SAD + 2*P2 <= 32767 (always true for block <= 15 at the node defaults).
 #include "sgm_device.h"
 
@@ -183,6 +184,45 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
     }
 }
 
+// DPL consecutive int16 as vector accesses (DPL a power of two <= 32; aligned to min(2*DPL, 16) B)
+template <int DPL>
+__device__ __forceinline__ void load_i16(const int16_t* p, int16_t (&v)[DPL])
+{
+    if constexpr (DPL == 1) v[0] = *p;
+    else if constexpr (DPL == 2) { const uint32_t w = *(const uint32_t*)p; v[0] = (int16_t)w; v[1] = (int16_t)(w >> 16); }
+    else {
+        constexpr int NW = DPL / 2;
+        uint32_t w[NW];
+        if constexpr (DPL == 4) { const uint2 t = *(const uint2*)p; w[0] = t.x; w[1] = t.y; }
+        else {
+#pragma unroll
+            for (int c = 0; c < NW / 4; c++) {
+                const uint4 t = ((const uint4*)p)[c];
+                w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NW; i++) { v[2 * i] = (int16_t)w[i]; v[2 * i + 1] = (int16_t)(w[i] >> 16); }
+    }
+}
+template <int DPL>
+__device__ __forceinline__ void store_i16(int16_t* p, const int (&v)[DPL])
+{
+    if constexpr (DPL == 1) *p = (int16_t)v[0];
+    else {
+        constexpr int NW = DPL / 2;
+        uint32_t w[NW];
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = ((uint32_t)v[2 * i] & 0xFFFFu) | ((uint32_t)v[2 * i + 1] << 16);
+        if constexpr (DPL == 2) *(uint32_t*)p = w[0];
+        else if constexpr (DPL == 4) *(uint2*)p = make_uint2(w[0], w[1]);
+        else {
+#pragma unroll
+            for (int c = 0; c < NW / 4; c++) ((uint4*)p)[c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+        }
+    }
+}
+
 // OpenCV recurrence of one cell with int16 storage semantics. Lanes/entries with d >= D
 // hold kMaxCost (acts as OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
 template <int DPL>
@@ -249,10 +289,15 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // C of the next PF steps in flight (one global-load latency per PF steps, not per step)
     constexpr int PF = 4;
     int Cb[PF][DPL];
+    // one vector load per lane (lanes past D read the last valid group and drop it): no
+    // exec-masked branch around the loads, so the prefetch keeps counted waits
+    const bool lane_act = lane * DPL < g.D;
+    const int dl = min(lane * DPL, g.D - DPL);
     auto load = [&](int (&c)[DPL], int i) {
-        const size_t o = cell(i);
+        int16_t v[DPL];
+        load_i16<DPL>(C + cell(i) + dl, v);
 #pragma unroll
-        for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; c[k] = d < g.D ? C[o + d] : 0; }
+        for (int k = 0; k < DPL; k++) c[k] = lane_act ? (int)v[k] : 0;
     };
 #pragma unroll
     for (int q = 0; q < PF; q++) load(Cb[q], q);
@@ -264,8 +309,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                 const size_t o = cell(i);
                 int L[DPL];
                 const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, lane, g, L);
-#pragma unroll
-                for (int k = 0; k < DPL; k++) { const int d = lane * DPL + k; if (d < g.D) V[o + d] = (int16_t)L[k]; }
+                if (lane_act) store_i16<DPL>(V + o + dl, L);
                 mLp = (int)(int16_t)wave_min(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];
@@ -276,38 +320,76 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     }
 }
 
-// one workgroup (4 waves) per row, each wave a group of 4 pixels in turn: S = saturate(sum L)
-// then the shared batched WTA + row epilogue
-template <int DPL>
-__global__ __launch_bounds__(256) void k_ocv_wta(const int16_t* __restrict__ vols, size_t vol_elems, int ndir, Geom g,
-                                                 int16_t* __restrict__ out, size_t out_stride)
+// WTA of the OCV modes, one workgroup (4 waves) per image row, 16 lanes per pixel (4 pixels
+// per wave-instruction): lane p of a row holds d = p*DPL .. p*DPL + DPL - 1 of its pixel,
+// loaded as one DPL x int16 vector per volume (coalesced). Same decisions as OpenCV's loop
+// (SURVEY Appendix A.6): S = saturate(sum of the NDIR L's); best = first minimal d through
+// one 16-lane min over (S + 32768) * 512 + d; uniqueness per element (S may be any int16
+// here); S[best +- 1] through a per-row LDS slice; then the shared disp2 / LR epilogue.
+template <int DPL, int NDIR>
+__global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ vols, size_t vol_elems, Geom g,
+                                                   int16_t* __restrict__ out, size_t out_stride)
 {
     extern __shared__ uint32_t lds_ocv[];
-    RowLds R(lds_ocv, g.W);
+    int16_t* sl = (int16_t*)lds_ocv;                      // 16 lane rows x 16 lanes x DPL S values
+    RowLds R((char*)lds_ocv + (size_t)16 * 16 * DPL * 2, g.W);
     const int tid = threadIdx.x, lane = tid & 63, y = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane >> 4, p = lane & 15;
     R.init(g, tid, 256);
-    for (int i0 = 4 * w; i0 < g.width1; i0 += 16) {
-        int S[4][DPL], xs[4], nvalid = 0;
+    const bool lane_act = p * DPL < g.D;
+    const int dl = lane_act ? p * DPL : 0;
+    int16_t* srow = sl + (w * 4 + r) * 16 * DPL;
+    const int n = g.width1, nq = (n + 3) / 4;
+    const size_t row0 = (size_t)y * g.width1 * g.D;
+    // pixel 4q + r; the last group reads up to 3 pixels past the row (the next row or the
+    // volume slack), results never stored
+    auto load = [&](int q, int16_t (&v)[NDIR][DPL]) {
+        const int16_t* base = vols + row0 + (size_t)(4 * q + r) * g.D + dl;
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int x1 = g.width1 - 1 - (i0 + u);
-            xs[u] = x1 + g.minX1;
+        for (int k = 0; k < NDIR; k++) load_i16<DPL>(base + (size_t)k * vol_elems, v[k]);
+    };
+    int16_t nxt[NDIR][DPL];
+    load(min(w, nq - 1), nxt);
+    for (int q = w; q < nq; q += 4) {
+        int S[DPL];
 #pragma unroll
-            for (int k = 0; k < DPL; k++) S[u][k] = 1 << 20;
-            if (x1 < 0) continue;
-            nvalid = u + 1;
-            const size_t o = ((size_t)y * g.width1 + x1) * g.D;
+        for (int k = 0; k < DPL; k++) {
+            int s = 0;
 #pragma unroll
-            for (int k = 0; k < DPL; k++) {
-                const int d = lane * DPL + k;
-                if (d >= g.D) continue;
-                int s = 0;
-                for (int r = 0; r < ndir; r++) s += vols[(size_t)r * vol_elems + o + d];
-                S[u][k] = min(max(s, -32768), kMaxCost);
-            }
+            for (int v = 0; v < NDIR; v++) s += nxt[v][k];
+            S[k] = min(max(s, -32768), 32767);
         }
-        wta_batch<DPL, 4>(S, lane, xs, nvalid, g, R.drow, R.bst, R.mins);
+        load(min(q + 4, nq - 1), nxt);
+        uint32_t km = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = p * DPL + k;
+            const uint32_t key = ((uint32_t)(S[k] + 32768) << 9) | (uint32_t)d;
+            km = (lane_act && d < g.D) ? min(km, key) : km;
+        }
+        const uint32_t kmin = row_min_u32(km);
+        const int best = (int)(kmin & 511u);
+        const int minS = (int)(kmin >> 9) - 32768;
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = p * DPL + k;
+            hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
+        }
+        const bool rej = row_sum_u32(hit ? 1u : 0u) != 0u;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) srow[p * DPL + k] = (int16_t)S[k];
+        const int sm = srow[max(best - 1, 0)], sp = srow[min(best + 1, g.D - 1)];
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const int x1 = 4 * q + r;
+        const bool wr = p == 0 && x1 < n;
+        const int x = wr ? g.minX1 + x1 : g.W + lane;
+        R.bst[x] = (int16_t)(rej ? -1 : best);
+        R.mins[x] = (uint16_t)minS;
+        R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
     }
     row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
@@ -354,16 +436,26 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
     return hipGetLastError();
 }
 
+template <int DPL>
+static void launch_ocv_wta_dpl(const int16_t* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+                               size_t out_stride, hipStream_t st)
+{
+    const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
+    if (ndir == 8)
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8>), dim3(g.H), dim3(256), lds, st, vols, vol_elems, g, out, out_stride);
+    else
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5>), dim3(g.H), dim3(256), lds, st, vols, vol_elems, g, out, out_stride);
+}
+
 hipError_t launch_ocv_wta(const int16_t* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
                           size_t out_stride, hipStream_t st)
 {
-    const size_t lds = RowLds::bytes(g.W);
-    switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_ocv_wta<1>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    case 2: hipLaunchKernelGGL(k_ocv_wta<2>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    case 4: hipLaunchKernelGGL(k_ocv_wta<4>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    default: hipLaunchKernelGGL(k_ocv_wta<8>, dim3(g.H), dim3(256), lds, st, vols, vol_elems, ndir, g, out, out_stride); break;
-    }
+    const int D = g.D;
+    if (D <= 32) launch_ocv_wta_dpl<2>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 64) launch_ocv_wta_dpl<4>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 128) launch_ocv_wta_dpl<8>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 256) launch_ocv_wta_dpl<16>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_dpl<32>(vols, vol_elems, ndir, g, out, out_stride, st);
     return hipGetLastError();
 }
 
