@@ -9,7 +9,8 @@
 //   k_ocv_vsum_seg   vertical box + P2 offset + OpenCV's bottom-row quirk:
 //                    rows with y + SH2 >= H are never recomputed (MODE_SGBM keeps the
 //                    last computed row, MODE_HH keeps the P2 initialisation)
-//   k_ocv_paths      each direction independently (L depends only on its own path);
+//   k_ocv_paths      each direction independently (L depends only on its own path), four
+//                    lines per wave (16 lanes each);
 //                    int16 storage of L and minL as OpenCV's CostType
 //   k_ocv_wta16      S = saturate(sum of L) (all L >= 0 inside the parity domain, so the
 //                    saturating order is irrelevant), 16 lanes per pixel, + the shared
@@ -20,6 +21,9 @@
 namespace sgm {
 
 constexpr int kMaxCost = 32767;
+#ifndef SGM_OCV_PF
+#define SGM_OCV_PF 8       // cost rows in flight per path line (D <= 64)
+#endif
 
 __global__ __launch_bounds__(256) void k_ocv_prefilter(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                        size_t stride, int W, int H, int ftzero,
@@ -223,20 +227,21 @@ __device__ __forceinline__ void store_i16(int16_t* p, const int (&v)[DPL])
     }
 }
 
-// OpenCV recurrence of one cell with int16 storage semantics. Lanes/entries with d >= D
-// hold kMaxCost (acts as OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
+// OpenCV recurrence of one cell with int16 storage semantics, for a path line held by the
+// 16 lanes of one row of the wave (lane p: d = p*DPL .. p*DPL + DPL - 1). Entries with
+// d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
 template <int DPL>
-__device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DPL], int mLp, bool pv, int lane,
+__device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DPL], int mLp, bool pv, int p,
                                         const Geom& g, int (&Lout)[DPL])
 {
-    const int fromLeft = dpp_shr1(Lp[DPL - 1], kMaxCost);
-    const int fromRight = dpp_shl1(Lp[0], kMaxCost);
+    const int fromLeft = (int)row_shr1((uint32_t)Lp[DPL - 1], (uint32_t)kMaxCost);
+    const int fromRight = (int)row_shl1((uint32_t)Lp[0], (uint32_t)kMaxCost);
     const int lp_min = pv ? mLp : 0;
     const int delta = lp_min + g.P2;
     int lmin = 1 << 30;
 #pragma unroll
     for (int k = 0; k < DPL; k++) {
-        const int d = lane * DPL + k;
+        const int d = p * DPL + k;
         int a = pv ? Lp[k] : 0;
         int lm1 = k > 0 ? Lp[k - 1] : fromLeft;
         int lp1 = k < DPL - 1 ? Lp[k + 1] : fromRight;
@@ -248,14 +253,27 @@ __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DP
     return lmin;
 }
 
-// One wave per line. Row sweeps (ry != 0): line = (column at step 0) for every line
-// start; horizontal (ry == 0): line = row.
+// signed min over the 16 lanes of each row, result in every lane of the row
+__device__ __forceinline__ int row_min_i32(int v)
+{
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));     // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));     // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, true));    // row_ror:4
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, true));    // row_ror:8
+    return v;
+}
+
+// Four path lines per wave, one per 16-lane row. Block b of direction dir holds its lines
+// 4b .. 4b+3: horizontal (ry == 0) line = row; row sweeps (ry != 0): lines [0, width1)
+// start on the first row at that column, the others on the entry column at row offset
+// line - width1 + 1. The lines of a block have (nearly) equal lengths; each stores only
+// while its own steps last.
 template <int DPL>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, int16_t* __restrict__ vols,
                                                   size_t vol_elems, Geom g, int dirmask, int4 nblk0, int4 nblk1)
 {
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
-    // block -> (direction, line); volume slot = rank of the direction in dirmask
+    // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
     int b = blockIdx.x, dir = 0, slot = 0;
     for (int i = 0; i < 8; i++) {
         if (!((dirmask >> i) & 1)) continue;
@@ -264,35 +282,39 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         slot++;
     }
     int16_t* V = vols + (size_t)slot * vol_elems;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, r = lane >> 4, p = lane & 15;
     const int rx = dir_rx(dir), ry = dir_ry(dir);
+    const int line = 4 * b + r;
+    const int nlines = ry == 0 ? g.H : g.width1 + (rx != 0 ? g.H - 1 : 0);
+    int x0 = 0, s0 = 0, n = 0;
+    if (line < nlines) {
+        if (ry == 0) { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = line; n = g.width1; }
+        else {
+            if (line < g.width1) { x0 = line; s0 = 0; }
+            else { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = line - g.width1 + 1; }
+            n = g.H - s0;
+            if (rx > 0) n = min(n, g.width1 - x0);
+            if (rx < 0) n = min(n, x0 + 1);
+        }
+    }
+    const int nmax = max(max(__builtin_amdgcn_readlane(n, 0), __builtin_amdgcn_readlane(n, 16)),
+                         max(__builtin_amdgcn_readlane(n, 32), __builtin_amdgcn_readlane(n, 48)));
+    auto cell = [&](int i) -> size_t {           // cell offset of step i (clamped to the line)
+        i = max(min(i, n - 1), 0);
+        const int y = ry == 0 ? s0 : (ry > 0 ? s0 + i : g.H - 1 - (s0 + i));
+        return ((size_t)y * g.width1 + (x0 + rx * i)) * g.D;
+    };
     int Lp[DPL], mLp = 0;
     bool pv = false;
 #pragma unroll
     for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
-    // The line as (x1, y) at step i: horizontal (ry == 0) = row b; row sweeps start on the
-    // first row at column b (b < width1) or on the entry column at row offset b - width1 + 1
-    int x0, s0, n;
-    if (ry == 0) { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = b; n = g.width1; }
-    else {
-        if (b < g.width1) { x0 = b; s0 = 0; }
-        else { x0 = rx > 0 ? 0 : g.width1 - 1; s0 = b - g.width1 + 1; }
-        n = g.H - s0;
-        if (rx > 0) n = min(n, g.width1 - x0);
-        if (rx < 0) n = min(n, x0 + 1);
-    }
-    auto cell = [&](int i) -> size_t {           // cell offset of step i (clamped to the line)
-        i = min(i, n - 1);
-        const int y = ry == 0 ? s0 : (ry > 0 ? s0 + i : g.H - 1 - (s0 + i));
-        return ((size_t)y * g.width1 + (x0 + rx * i)) * g.D;
-    };
-    // C of the next PF steps in flight (one global-load latency per PF steps, not per step)
-    constexpr int PF = 4;
-    int Cb[PF][DPL];
+    // C of the next PF steps in flight (one global-load latency per PF steps, not per step);
     // one vector load per lane (lanes past D read the last valid group and drop it): no
     // exec-masked branch around the loads, so the prefetch keeps counted waits
-    const bool lane_act = lane * DPL < g.D;
-    const int dl = min(lane * DPL, g.D - DPL);
+    constexpr int PF = DPL <= 4 ? SGM_OCV_PF : 4;
+    int Cb[PF][DPL];
+    const bool lane_act = p * DPL < g.D;
+    const int dl = min(p * DPL, g.D - DPL);
     auto load = [&](int (&c)[DPL], int i) {
         int16_t v[DPL];
         load_i16<DPL>(C + cell(i) + dl, v);
@@ -301,16 +323,16 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     };
 #pragma unroll
     for (int q = 0; q < PF; q++) load(Cb[q], q);
-    for (int i0 = 0; i0 < n; i0 += PF) {
+    for (int i0 = 0; i0 < nmax; i0 += PF) {
 #pragma unroll
         for (int q = 0; q < PF; q++) {
             const int i = i0 + q;
-            if (i < n) {                          // wave-uniform
+            if (i < nmax) {                       // wave-uniform
                 const size_t o = cell(i);
                 int L[DPL];
-                const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, lane, g, L);
-                if (lane_act) store_i16<DPL>(V + o + dl, L);
-                mLp = (int)(int16_t)wave_min(lmin);   // minLr is CostType
+                const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, p, g, L);
+                if (lane_act && i < n) store_i16<DPL>(V + o + dl, L);
+                mLp = (int)(int16_t)row_min_i32(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];
                 pv = true;
@@ -395,7 +417,7 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ v
 }
 
 // ------------------------------------------------------------------------------------
-static int dpl_for(int D) { return D <= 64 ? 1 : D <= 128 ? 2 : D <= 256 ? 4 : 8; }
+static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
 hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, const Geom& g, int fullDP,
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
@@ -423,7 +445,8 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
     for (int i = 0; i < 8; i++) {
         nb[i] = 0;
         if (!((dirmask >> i) & 1)) continue;
-        nb[i] = dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0);
+        const int lines = dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0);
+        nb[i] = (lines + 3) / 4;                   // 4 lines per wave
         total += nb[i];
     }
     int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
@@ -431,7 +454,9 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
     case 1: hipLaunchKernelGGL(k_ocv_paths<1>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
     case 2: hipLaunchKernelGGL(k_ocv_paths<2>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
     case 4: hipLaunchKernelGGL(k_ocv_paths<4>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    default: hipLaunchKernelGGL(k_ocv_paths<8>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
+    case 8: hipLaunchKernelGGL(k_ocv_paths<8>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
+    case 16: hipLaunchKernelGGL(k_ocv_paths<16>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
+    default: hipLaunchKernelGGL(k_ocv_paths<32>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
     }
     return hipGetLastError();
 }

@@ -82,32 +82,77 @@ __device__ __forceinline__ void uf_union(int* __restrict__ lab, int a, int b)
     }
 }
 
-__global__ __launch_bounds__(256) void k_spk_init(const int16_t* __restrict__ d, size_t stride, int W, int H,
-                                                  int newVal, int* __restrict__ lab, int* __restrict__ cnt)
+// Phase 1, one 64 x 16 tile per block: union-find of the tile's own edges in LDS (local
+// index = ty * 64 + tx, same order as the global raster index), then every pixel's global
+// label = the global index of its tile-local root (<= its own index: the invariant holds).
+constexpr int kSpkTW = 64, kSpkTH = 16;
+__device__ __forceinline__ int luf_find(int* l, int x)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= W * H) return;
-    const int y = i / W, x = i - y * W;
-    lab[i] = d[(size_t)y * stride + x] != newVal ? i : -1;
-    cnt[i] = 0;
+    int p = l[x];
+    while (p != x) { const int q = l[p]; if (q != p) atomicMin(&l[x], q); x = p; p = q; }
+    return x;
+}
+__device__ __forceinline__ void luf_union(int* l, int a, int b)
+{
+    for (;;) {
+        a = luf_find(l, a);
+        b = luf_find(l, b);
+        if (a == b) return;
+        if (a < b) { int t = a; a = b; b = t; }
+        const int old = atomicMin(&l[a], b);
+        if (old == a) return;
+        a = old;
+    }
+}
+__global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d, size_t stride, int W, int H,
+                                                  int newVal, int maxDiff, int* __restrict__ lab, int* __restrict__ cnt)
+{
+    __shared__ int l[kSpkTW * kSpkTH];
+    __shared__ int16_t v[kSpkTW * kSpkTH];
+    const int x0 = blockIdx.x * kSpkTW, y0 = blockIdx.y * kSpkTH;
+    for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
+        const int x = x0 + (i & (kSpkTW - 1)), y = y0 + i / kSpkTW;
+        const int dv = (x < W && y < H) ? d[(size_t)y * stride + x] : newVal;
+        v[i] = (int16_t)dv;
+        l[i] = dv != newVal ? i : -1;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
+        const int tx = i & (kSpkTW - 1), ty = i / kSpkTW;
+        const int a = v[i];
+        if (a == newVal) continue;
+        if (tx + 1 < kSpkTW) { const int q = v[i + 1]; if (q != newVal && abs(a - q) <= maxDiff) luf_union(l, i, i + 1); }
+        if (ty + 1 < kSpkTH) { const int q = v[i + kSpkTW]; if (q != newVal && abs(a - q) <= maxDiff) luf_union(l, i, i + kSpkTW); }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
+        const int x = x0 + (i & (kSpkTW - 1)), y = y0 + i / kSpkTW;
+        if (x >= W || y >= H) continue;
+        int r = -1;
+        if (l[i] >= 0) {
+            r = i;
+            while (l[r] != r) r = l[r];
+            r = (y0 + r / kSpkTW) * W + x0 + (r & (kSpkTW - 1));
+        }
+        lab[y * W + x] = r;
+        cnt[y * W + x] = 0;
+    }
 }
 
-__global__ __launch_bounds__(256) void k_spk_union(const int16_t* __restrict__ d, size_t stride, int W, int H,
-                                                   int newVal, int maxDiff, int* __restrict__ lab)
+// Phase 2: the edges that cross tile borders (right column and bottom row of each tile),
+// merged with the global union-find.
+__global__ __launch_bounds__(256) void k_spk_border(const int16_t* __restrict__ d, size_t stride, int W, int H,
+                                                    int newVal, int maxDiff, int* __restrict__ lab)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= W * H) return;
-    const int y = i / W, x = i - y * W;
-    const int v = d[(size_t)y * stride + x];
-    if (v == newVal) return;
-    if (x + 1 < W) {
-        const int q = d[(size_t)y * stride + x + 1];
-        if (q != newVal && abs(v - q) <= maxDiff) uf_union(lab, i, i + 1);
-    }
-    if (y + 1 < H) {
-        const int q = d[(size_t)(y + 1) * stride + x];
-        if (q != newVal && abs(v - q) <= maxDiff) uf_union(lab, i, i + W);
-    }
+    const int x0 = blockIdx.x * kSpkTW, y0 = blockIdx.y * kSpkTH;
+    const int t = threadIdx.x;
+    int x, y, dx, dy;
+    if (t < kSpkTH) { x = x0 + kSpkTW - 1; y = y0 + t; dx = 1; dy = 0; }             // right edge
+    else if (t < kSpkTH + kSpkTW) { x = x0 + t - kSpkTH; y = y0 + kSpkTH - 1; dx = 0; dy = 1; }  // bottom edge
+    else return;
+    if (x + dx >= W || y + dy >= H || x >= W || y >= H) return;
+    const int a = d[(size_t)y * stride + x], q = d[(size_t)(y + dy) * stride + x + dx];
+    if (a != newVal && q != newVal && abs(a - q) <= maxDiff) uf_union(lab, y * W + x, (y + dy) * W + x + dx);
 }
 
 // After the union phase (a kernel boundary away): every label points straight at its root.
@@ -153,8 +198,9 @@ hipError_t launch_speckle(int16_t* d, size_t stride, int W, int H, int newVal, i
 {
     const int n = W * H;
     dim3 grid((n + 255) / 256), block(256);
-    hipLaunchKernelGGL(k_spk_init, grid, block, 0, st, d, stride, W, H, newVal, lab, cnt);
-    hipLaunchKernelGGL(k_spk_union, grid, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
+    const dim3 tiles((W + kSpkTW - 1) / kSpkTW, (H + kSpkTH - 1) / kSpkTH);
+    hipLaunchKernelGGL(k_spk_tile, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab, cnt);
+    hipLaunchKernelGGL(k_spk_border, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
     hipLaunchKernelGGL(k_spk_flatten, grid, block, 0, st, W, H, lab);
     hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, lab, cnt);
     hipLaunchKernelGGL(k_spk_apply, grid, block, 0, st, d, stride, W, H, newVal, maxSize, lab, cnt);

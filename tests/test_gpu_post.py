@@ -30,3 +30,29 @@ def test_speckles_one_giant_component(engine, oracle):
     out = engine.filter_speckles(d, -16, 100, 16)
     assert np.array_equal(out, oracle.filter_speckles(d, -16, 100, 16))
     assert (out[500:510, 900:910] == -16).all()
+
+
+@pytest.mark.parametrize("shape", [(37, 101), (1, 300), (300, 1), (17, 130), (65, 64)])
+def test_speckles_ragged_tiles(engine, oracle, shape):
+    """Image sizes that cut the 64 x 16 union-find tiles: components crossing partial tiles."""
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1])
+    d = (rng.integers(0, 3, shape) * 16).astype(np.int16)
+    d[rng.random(shape) < 0.15] = -16
+    for max_size in (0, 3, 40):
+        assert np.array_equal(engine.filter_speckles(d, -16, max_size, 16),
+                              oracle.filter_speckles(d, -16, max_size, 16)), max_size
+
+
+def test_speckles_serpentine(engine, oracle):
+    """One long serpentine component winding through many tiles (border merges chained
+    over the whole image), beside small isolated blobs."""
+    h, w = 96, 200
+    d = np.full((h, w), -16, np.int16)
+    for r in range(0, h, 4):
+        d[r, 1:w - 1] = 64
+        c = w - 2 if (r // 4) % 2 == 0 else 1
+        d[r:r + 4, c] = 64
+    d[2::8, 5::9] = 400
+    for max_size in (1, 500, 5000):
+        assert np.array_equal(engine.filter_speckles(d, -16, max_size, 16),
+                              oracle.filter_speckles(d, -16, max_size, 16)), max_size
