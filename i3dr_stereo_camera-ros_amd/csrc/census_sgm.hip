@@ -927,17 +927,10 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
     if (n > cap) return -1;
     std::stable_sort(v.begin(), v.end(), [](const Item& a, const Item& b) { return a.len > b.len; });
     n_slots = std::max(n_slots, 1);
-    // XCD-aware placement (SGM_XCD_DEAL=1): blocks are dealt round-robin over the 8 XCDs, so
-    // slot j of a full round goes to block (j % per) * 8 + j / per: runs of `per` consecutive
-    // items (adjacent column blocks of one direction, whose row segments overlap) share an XCD
-    // and its L2.
-    static const int xcd = getenv("SGM_XCD_DEAL") ? atoi(getenv("SGM_XCD_DEAL")) : 0;
     for (int k = 0; k < n; k++) {
         const int round = k / n_slots, i = k % n_slots;
         const int in_round = std::min(n_slots, n - round * n_slots);
-        int pos = (round & 1) ? in_round - 1 - i : i;
-        if (xcd && in_round == n_slots && n_slots % 8 == 0) pos = (pos % (n_slots / 8)) * 8 + pos / (n_slots / 8);
-        out[round * n_slots + pos] = v[k].code;
+        out[round * n_slots + ((round & 1) ? in_round - 1 - i : i)] = v[k].code;
     }
     return n;
 }

@@ -130,8 +130,10 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         br[(c * 3 + 0) * NR + r] = (uint8_t)v; br[(c * 3 + 1) * NR + r] = (uint8_t)lo; br[(c * 3 + 2) * NR + r] = (uint8_t)hi;
     }
     __syncthreads();
+    // (k, d) of flat index i = k * D + d, advanced by 256 per iteration without divisions
+    const int kstep = 256 / g.D, dstep = 256 - kstep * g.D;
+    int k = tid / g.D, d = tid - k * g.D;
     for (int i = tid; i < NX * g.D; i += 256) {
-        const int k = i / g.D, d = i - k * g.D;
         const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
         const int r = x - g.minD - d - xr0;                // index of xr = x - minD - d
         int acc = 0;
@@ -144,14 +146,16 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
             acc += min(c0, c1) >> (c == 0 ? 0 : 2);
         }
         P[i] = (int16_t)acc;
+        k += kstep; d += dstep;
+        if (d >= g.D) { d -= g.D; k++; }
     }
     __syncthreads();
     const int nout = min(kPixXB, g.width1 - x0);
+    int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D;     // the block's outputs are contiguous
     for (int i = tid; i < nout * g.D; i += 256) {
-        const int xo = i / g.D, d = i - xo * g.D;
         int sum = 0;
-        for (int k = 0; k <= 2 * SW2; k++) sum += P[(xo + k) * g.D + d];
-        hs[((size_t)y * g.width1 + x0 + xo) * g.D + d] = (int16_t)sum;
+        for (int t = 0; t <= 2 * SW2; t++) sum += P[i + t * g.D];   // P[(xo + t) * D + d], i = xo * D + d
+        dst[i] = (int16_t)sum;
     }
 }
 
