@@ -14,6 +14,12 @@
 #ifndef SGM_WPE
 #define SGM_WPE 4          // minimum waves per SIMD of the path kernels (register budget)
 #endif
+#ifndef SGM_NT_STORE
+#define SGM_NT_STORE 1     // path volumes written with nontemporal stores (0: plain)
+#endif
+#ifndef SGM_NT_LOAD
+#define SGM_NT_LOAD 1      // WTA volume loads with the nt cache policy (0: default)
+#endif
 #ifndef SGM_ROWS_LPL8
 #define SGM_ROWS_LPL8 0    // 1: row sweeps with 8 lanes per path line for D <= 256 (RowsCfg; measured slower)
 #endif
@@ -99,15 +105,16 @@ template <int DPL>
 __device__ __forceinline__ void wload_buf(const uint8_t* base, uint32_t off, uint32_t (&wd)[(DPL + 3) / 4])
 {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
-    if constexpr (DPL == 2) { wd[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0); }
-    else if constexpr (DPL == 4) { wd[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0); }
+    constexpr int aux = SGM_NT_LOAD ? 2 : 0;           // 2: nt (streamed once)
+    if constexpr (DPL == 2) { wd[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, aux); }
+    else if constexpr (DPL == 4) { wd[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, aux); }
     else if constexpr (DPL == 8) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, aux);
         wd[0] = v[0]; wd[1] = v[1];
     } else {
 #pragma unroll
         for (int q = 0; q < DPL / 16; q++) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * q, 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * q, 0, aux);
             wd[4 * q] = v[0]; wd[4 * q + 1] = v[1]; wd[4 * q + 2] = v[2]; wd[4 * q + 3] = v[3];
         }
     }
@@ -127,12 +134,17 @@ __device__ __forceinline__ void store_pairs(uint8_t* dst, uint8_t* dst_hi, const
         *(uint2*)dst = make_uint2(__builtin_amdgcn_perm(L[1], L[0], 0x06040200u),
                                   __builtin_amdgcn_perm(L[3], L[2], 0x06040200u));
     } else {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int q = 0; q < DPL / 16; q++)
-            *(uint4*)(q == 0 ? dst : dst_hi) = make_uint4(__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
-                                          __builtin_amdgcn_perm(L[8 * q + 3], L[8 * q + 2], 0x06040200u),
-                                          __builtin_amdgcn_perm(L[8 * q + 5], L[8 * q + 4], 0x06040200u),
-                                          __builtin_amdgcn_perm(L[8 * q + 7], L[8 * q + 6], 0x06040200u));
+        for (int q = 0; q < DPL / 16; q++) {
+            const v4u v = {__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
+                           __builtin_amdgcn_perm(L[8 * q + 3], L[8 * q + 2], 0x06040200u),
+                           __builtin_amdgcn_perm(L[8 * q + 5], L[8 * q + 4], 0x06040200u),
+                           __builtin_amdgcn_perm(L[8 * q + 7], L[8 * q + 6], 0x06040200u)};
+            v4u* d = (v4u*)(q == 0 ? dst : dst_hi);
+            if constexpr (SGM_NT_STORE) __builtin_nontemporal_store(v, d);
+            else *d = v;
+        }
     }
 }
 
