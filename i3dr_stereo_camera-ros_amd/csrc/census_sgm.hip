@@ -127,12 +127,18 @@ __device__ __forceinline__ void store_pairs(uint8_t* dst, uint8_t* dst_hi, const
 {
     // (lo, hi) u16 pairs with values <= 255 -> DPL consecutive bytes
     if constexpr (DPL == 2) {
-        *(uint16_t*)dst = (uint16_t)__builtin_amdgcn_perm(0u, L[0], 0x0c0c0200u);
+        const uint16_t v = (uint16_t)__builtin_amdgcn_perm(0u, L[0], 0x0c0c0200u);
+        if constexpr (SGM_NT_STORE) __builtin_nontemporal_store(v, (uint16_t*)dst);
+        else *(uint16_t*)dst = v;
     } else if constexpr (DPL == 4) {
-        *(uint32_t*)dst = __builtin_amdgcn_perm(L[1], L[0], 0x06040200u);
+        const uint32_t v = __builtin_amdgcn_perm(L[1], L[0], 0x06040200u);
+        if constexpr (SGM_NT_STORE) __builtin_nontemporal_store(v, (uint32_t*)dst);
+        else *(uint32_t*)dst = v;
     } else if constexpr (DPL == 8) {
-        *(uint2*)dst = make_uint2(__builtin_amdgcn_perm(L[1], L[0], 0x06040200u),
-                                  __builtin_amdgcn_perm(L[3], L[2], 0x06040200u));
+        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+        const v2u v = {__builtin_amdgcn_perm(L[1], L[0], 0x06040200u), __builtin_amdgcn_perm(L[3], L[2], 0x06040200u)};
+        if constexpr (SGM_NT_STORE) __builtin_nontemporal_store(v, (v2u*)dst);
+        else *(v2u*)dst = v;
     } else {
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
