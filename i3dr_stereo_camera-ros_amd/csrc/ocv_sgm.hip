@@ -213,20 +213,24 @@ __device__ __forceinline__ void load_i16(const int16_t* p, int16_t (&v)[DPL])
         for (int i = 0; i < NW; i++) { v[2 * i] = (int16_t)w[i]; v[2 * i + 1] = (int16_t)(w[i] >> 16); }
     }
 }
+// nontemporal: the path volumes are streamed once into the WTA
 template <int DPL>
 __device__ __forceinline__ void store_i16(int16_t* p, const int (&v)[DPL])
 {
-    if constexpr (DPL == 1) *p = (int16_t)v[0];
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (DPL == 1) __builtin_nontemporal_store((int16_t)v[0], p);
     else {
         constexpr int NW = DPL / 2;
         uint32_t w[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) w[i] = ((uint32_t)v[2 * i] & 0xFFFFu) | ((uint32_t)v[2 * i + 1] << 16);
-        if constexpr (DPL == 2) *(uint32_t*)p = w[0];
-        else if constexpr (DPL == 4) *(uint2*)p = make_uint2(w[0], w[1]);
+        if constexpr (DPL == 2) __builtin_nontemporal_store(w[0], (uint32_t*)p);
+        else if constexpr (DPL == 4) __builtin_nontemporal_store((v2u){w[0], w[1]}, (v2u*)p);
         else {
 #pragma unroll
-            for (int c = 0; c < NW / 4; c++) ((uint4*)p)[c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+            for (int c = 0; c < NW / 4; c++)
+                __builtin_nontemporal_store((v4u){w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]}, (v4u*)p + c);
         }
     }
 }
