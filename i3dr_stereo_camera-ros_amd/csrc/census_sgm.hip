@@ -1052,10 +1052,12 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
     const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * rows_lds_codes<DPL>(),
                                  (size_t)(kCensusRows + 6) * 72});
     uint64_t* tr = trace_buffer((int)grid.x);
-    // WTA rows interleaved one per 2.75 blocks (C3 sweep: after the paths 554 pairs/s, 1/2 498,
-    // 1/2.5 578, 1/2.75 580, 1/3 577, 1/3.5 574): the HBM-bound rows co-run with the
-    // VALU-bound sweeps on ~1 slot in 4 instead of waiting for the sweeps' tail
-    static const int period = getenv("SGM_WTA_PERIOD") ? (int)(16 * atof(getenv("SGM_WTA_PERIOD"))) : 44;
+    // WTA rows interleaved one per 2.5 blocks (C3 sweeps, first build: after the paths 554
+    // pairs/s, 1/2 498, 1/2.5 578, 1/2.75 580, 1/3 577, 1/3.5 574; with nontemporal volumes,
+    // two interleaved rounds: 1/2.25 655-658, 1/2.5 660-663, 1/2.75 641-657, 1/3.25 649-652,
+    // 1/4 621-635): the memory-bound rows co-run with the VALU-bound sweeps on ~1 slot in 3
+    // instead of waiting for the sweeps' tail
+    static const int period = getenv("SGM_WTA_PERIOD") ? (int)(16 * atof(getenv("SGM_WTA_PERIOD"))) : 40;
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
                            pl, items, n_items, out_stride, period, tr);
