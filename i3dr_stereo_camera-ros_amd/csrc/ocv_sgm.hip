@@ -278,7 +278,8 @@ __device__ __forceinline__ int row_min_i32(int v)
 // while its own steps last.
 template <int DPL>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, int16_t* __restrict__ vols,
-                                                  size_t vol_elems, Geom g, int dirmask, int4 nblk0, int4 nblk1)
+                                                  size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
+                                                  int4 nblk1)
 {
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
     // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
@@ -307,11 +308,12 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     }
     const int nmax = max(max(__builtin_amdgcn_readlane(n, 0), __builtin_amdgcn_readlane(n, 16)),
                          max(__builtin_amdgcn_readlane(n, 32), __builtin_amdgcn_readlane(n, 48)));
-    auto cell = [&](int i) -> size_t {           // cell offset of step i (clamped to the line)
-        i = max(min(i, n - 1), 0);
-        const int y = ry == 0 ? s0 : (ry > 0 ? s0 + i : g.H - 1 - (s0 + i));
-        return ((size_t)y * g.width1 + (x0 + rx * i)) * g.D;
-    };
+    // cell offset of step i (clamped to the line) = base + i * step, branch-free
+    const int ybase = ry >= 0 ? s0 : g.H - 1 - s0;
+    const long long cbase = ((long long)ybase * g.width1 + x0) * g.D;
+    const long long cstep = ((long long)ry * g.width1 + rx) * g.D;
+    const int ilast = max(n - 1, 0);
+    auto cell = [&](int i) -> size_t { return (size_t)(cbase + (long long)min(i, ilast) * cstep); };
     int Lp[DPL], mLp = 0;
     bool pv = false;
 #pragma unroll
@@ -329,22 +331,25 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
 #pragma unroll
         for (int k = 0; k < DPL; k++) c[k] = lane_act ? (int)v[k] : 0;
     };
+    // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop):
+    // steps past a line's end and lanes past D store to a per-lane trash slot after the
+    // volumes (vols + trash_off).
+    int16_t* const tr = vols + trash_off + lane * DPL;
 #pragma unroll
     for (int q = 0; q < PF; q++) load(Cb[q], q);
     for (int i0 = 0; i0 < nmax; i0 += PF) {
 #pragma unroll
         for (int q = 0; q < PF; q++) {
             const int i = i0 + q;
-            if (i < nmax) {                       // wave-uniform
-                const size_t o = cell(i);
-                int L[DPL];
-                const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, p, g, L);
-                if (lane_act && i < n) store_i16<DPL>(V + o + dl, L);
-                mLp = (int)(int16_t)row_min_i32(lmin);   // minLr is CostType
+            int L[DPL];
+            const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, p, g, L);
+            const bool ok = lane_act && i < n;
+            const size_t o = cell(i) + dl;
+            store_i16<DPL>((int16_t*)((uintptr_t)(V + o) * ok + (uintptr_t)tr * !ok), L);
+            mLp = (int)(int16_t)row_min_i32(lmin);   // minLr is CostType
 #pragma unroll
-                for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-                pv = true;
-            }
+            for (int k = 0; k < DPL; k++) Lp[k] = L[k];
+            pv = true;
             load(Cb[q], i + PF);
         }
     }
@@ -446,9 +451,13 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
     return hipGetLastError();
 }
 
+// vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 int16 of trash slots
 hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
                             hipStream_t st)
 {
+    int ndir = 0;
+    for (int i = 0; i < 8; i++) ndir += (dirmask >> i) & 1;
+    const size_t trash_off = (size_t)ndir * vol_elems;
     int nb[8], total = 0;
     for (int i = 0; i < 8; i++) {
         nb[i] = 0;
@@ -459,12 +468,12 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
     }
     int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
     switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_ocv_paths<1>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    case 2: hipLaunchKernelGGL(k_ocv_paths<2>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    case 4: hipLaunchKernelGGL(k_ocv_paths<4>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    case 8: hipLaunchKernelGGL(k_ocv_paths<8>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    case 16: hipLaunchKernelGGL(k_ocv_paths<16>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
-    default: hipLaunchKernelGGL(k_ocv_paths<32>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, g, dirmask, a, b); break;
+    case 1: hipLaunchKernelGGL(k_ocv_paths<1>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    case 2: hipLaunchKernelGGL(k_ocv_paths<2>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    case 4: hipLaunchKernelGGL(k_ocv_paths<4>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    case 8: hipLaunchKernelGGL(k_ocv_paths<8>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    case 16: hipLaunchKernelGGL(k_ocv_paths<16>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    default: hipLaunchKernelGGL(k_ocv_paths<32>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
     }
     return hipGetLastError();
 }

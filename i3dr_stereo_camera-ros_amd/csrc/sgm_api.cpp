@@ -278,8 +278,9 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
         l.ovol_elems = align_up(cells * 2) / 2;
-        // + slack: the WTA's last pixel group of the last row reads 3 pixels past the volume
-        l.ovols = take(l.ovol_elems * 2 * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + (size_t)8 * g.D);
+        // + slack: the path kernel's trash slots (64 lanes x 32 int16) and the WTA's last pixel
+        // group of the last row, which reads 3 pixels past the volume
+        l.ovols = take(l.ovol_elems * 2 * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 4096 + (size_t)8 * g.D);
     }
     l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
