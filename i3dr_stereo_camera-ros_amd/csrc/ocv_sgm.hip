@@ -17,6 +17,7 @@
 //                    disp2 / LR row code.
 // Parity domain: SAD + 2*P2 <= 32767 (always true for block <= 15 at the node defaults).
 #include "sgm_device.h"
+#include <cstdlib>
 
 namespace sgm {
 
@@ -235,15 +236,29 @@ __device__ __forceinline__ void store_i16(int16_t* p, const int (&v)[DPL])
     }
 }
 
-// OpenCV recurrence of one cell with int16 storage semantics, for a path line held by the
-// 16 lanes of one row of the wave (lane p: d = p*DPL .. p*DPL + DPL - 1). Entries with
-// d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
-template <int DPL>
+// OpenCV recurrence of one cell with int16 storage semantics, for a path line held by LPL
+// lanes (16: one row of the wave; 32: two rows) — lane p: d = p*DPL .. p*DPL + DPL - 1.
+// Entries with d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
+template <int LPL>
+__device__ __forceinline__ int line_shr1(int v, int p)
+{
+    if constexpr (LPL == 16) return (int)row_shr1((uint32_t)v, (uint32_t)kMaxCost);
+    const int t = __builtin_amdgcn_update_dpp(kMaxCost, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    return p == 0 ? kMaxCost : t;                      // lane 32 must not see lane 31 (the other line)
+}
+template <int LPL>
+__device__ __forceinline__ int line_shl1(int v, int p)
+{
+    if constexpr (LPL == 16) return (int)row_shl1((uint32_t)v, (uint32_t)kMaxCost);
+    const int t = __builtin_amdgcn_update_dpp(kMaxCost, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
+    return p == LPL - 1 ? kMaxCost : t;
+}
+template <int DPL, int LPL>
 __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DPL], int mLp, bool pv, int p,
                                         const Geom& g, int (&Lout)[DPL])
 {
-    const int fromLeft = (int)row_shr1((uint32_t)Lp[DPL - 1], (uint32_t)kMaxCost);
-    const int fromRight = (int)row_shl1((uint32_t)Lp[0], (uint32_t)kMaxCost);
+    const int fromLeft = line_shr1<LPL>(Lp[DPL - 1], p);
+    const int fromRight = line_shl1<LPL>(Lp[0], p);
     const int lp_min = pv ? mLp : 0;
     const int delta = lp_min + g.P2;
     int lmin = 1 << 30;
@@ -261,22 +276,29 @@ __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DP
     return lmin;
 }
 
-// signed min over the 16 lanes of each row, result in every lane of the row
-__device__ __forceinline__ int row_min_i32(int v)
+// signed min over the LPL lanes of each line (16: a row; 32: a row pair joined by
+// v_permlane16_swap), result in every lane of the line
+template <int LPL>
+__device__ __forceinline__ int line_min_i32(int v)
 {
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));     // quad_perm [1,0,3,2]
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));     // quad_perm [2,3,0,1]
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, true));    // row_ror:4
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, true));    // row_ror:8
+    if constexpr (LPL == 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // rows (0,1), (2,3) exchanged
+        v = min((int)sw[0], (int)sw[1]);
+    }
     return v;
 }
 
-// Four path lines per wave, one per 16-lane row. Block b of direction dir holds its lines
-// 4b .. 4b+3: horizontal (ry == 0) line = row; row sweeps (ry != 0): lines [0, width1)
-// start on the first row at that column, the others on the entry column at row offset
+// 64 / LPL path lines per wave. Block b of direction dir holds its lines NLW*b .. NLW*b +
+// NLW - 1: horizontal (ry == 0) line = row; row sweeps (ry != 0): lines [0, width1) start on
+// the first row at that column, the others on the entry column at row offset
 // line - width1 + 1. The lines of a block have (nearly) equal lengths; each stores only
-// while its own steps last.
-template <int DPL>
+// while its own steps last. Fewer, wider lines (LPL 32) shorten each step's instruction
+// chain: a line is a sequential walk, and its step latency bounds the kernel.
+template <int DPL, int LPL>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, int16_t* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
                                                   int4 nblk1)
@@ -291,9 +313,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         slot++;
     }
     int16_t* V = vols + (size_t)slot * vol_elems;
-    const int lane = threadIdx.x, r = lane >> 4, p = lane & 15;
+    constexpr int NLW = 64 / LPL;                      // lines per wave
+    const int lane = threadIdx.x, r = lane / LPL, p = lane % LPL;
     const int rx = dir_rx(dir), ry = dir_ry(dir);
-    const int line = 4 * b + r;
+    const int line = NLW * b + r;
     const int nlines = ry == 0 ? g.H : g.width1 + (rx != 0 ? g.H - 1 : 0);
     int x0 = 0, s0 = 0, n = 0;
     if (line < nlines) {
@@ -306,8 +329,9 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             if (rx < 0) n = min(n, x0 + 1);
         }
     }
-    const int nmax = max(max(__builtin_amdgcn_readlane(n, 0), __builtin_amdgcn_readlane(n, 16)),
-                         max(__builtin_amdgcn_readlane(n, 32), __builtin_amdgcn_readlane(n, 48)));
+    int nmax = 0;
+#pragma unroll
+    for (int w = 0; w < NLW; w++) nmax = max(nmax, __builtin_amdgcn_readlane(n, w * LPL));
     // cell offset of step i (clamped to the line) = base + i * step, branch-free
     const int ybase = ry >= 0 ? s0 : g.H - 1 - s0;
     const long long cbase = ((long long)ybase * g.width1 + x0) * g.D;
@@ -342,11 +366,11 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         for (int q = 0; q < PF; q++) {
             const int i = i0 + q;
             int L[DPL];
-            const int lmin = ocv_step<DPL>(Cb[q], Lp, mLp, pv, p, g, L);
+            const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, pv, p, g, L);
             const bool ok = lane_act && i < n;
             const size_t o = cell(i) + dl;
             store_i16<DPL>((int16_t*)((uintptr_t)(V + o) * ok + (uintptr_t)tr * !ok), L);
-            mLp = (int)(int16_t)row_min_i32(lmin);   // minLr is CostType
+            mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
             for (int k = 0; k < DPL; k++) Lp[k] = L[k];
             pv = true;
@@ -452,8 +476,9 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 }
 
 // vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 int16 of trash slots
-hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
-                            hipStream_t st)
+template <int DPL, int LPL>
+static void launch_ocv_paths_l(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
+                               hipStream_t st)
 {
     int ndir = 0;
     for (int i = 0; i < 8; i++) ndir += (dirmask >> i) & 1;
@@ -463,17 +488,49 @@ hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, c
         nb[i] = 0;
         if (!((dirmask >> i) & 1)) continue;
         const int lines = dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0);
-        nb[i] = (lines + 3) / 4;                   // 4 lines per wave
+        nb[i] = (lines + 64 / LPL - 1) / (64 / LPL);
         total += nb[i];
     }
-    int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
-    switch (dpl_for(g.D)) {
-    case 1: hipLaunchKernelGGL(k_ocv_paths<1>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
-    case 2: hipLaunchKernelGGL(k_ocv_paths<2>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
-    case 4: hipLaunchKernelGGL(k_ocv_paths<4>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
-    case 8: hipLaunchKernelGGL(k_ocv_paths<8>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
-    case 16: hipLaunchKernelGGL(k_ocv_paths<16>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
-    default: hipLaunchKernelGGL(k_ocv_paths<32>, dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g, dirmask, a, b); break;
+    const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
+    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
+                       dirmask, a, b);
+}
+
+// Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
+// the latency of one step: 32 lanes halve the step's chain (D/32 cells per lane) at the
+// cost of a permlane16_swap and two masks per step. With enough lines to fill the SIMDs
+// the 16-lane step, fewer instructions per cell, wins (MI355X: C1 640x480 D=64 0.36 vs
+// 0.39-0.42 ms per frame; 1920x1080 D=128 3.24 vs 2.85 ms). SGM_OCV_LPL=16|32 forces one.
+constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lanes pay
+static int ocv_lanes_per_line(const Geom& g, int dirmask)
+{
+    if (g.D <= 32) return 16;
+    if (const char* e = getenv("SGM_OCV_LPL")) return atoi(e) == 32 ? 32 : 16;
+    int waves = 0;
+    for (int i = 0; i < 8; i++)
+        if ((dirmask >> i) & 1)
+            waves += ((dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0)) + 3) / 4;
+    return waves < kOcvWideLineWaves ? 32 : 16;
+}
+
+hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
+                            hipStream_t st)
+{
+    const int D = g.D;
+    if (ocv_lanes_per_line(g, dirmask) == 32) {
+        if (D <= 64) launch_ocv_paths_l<2, 32>(C, vols, vol_elems, g, dirmask, st);
+        else if (D <= 128) launch_ocv_paths_l<4, 32>(C, vols, vol_elems, g, dirmask, st);
+        else if (D <= 256) launch_ocv_paths_l<8, 32>(C, vols, vol_elems, g, dirmask, st);
+        else launch_ocv_paths_l<16, 32>(C, vols, vol_elems, g, dirmask, st);
+    } else {
+        switch (dpl_for(D)) {
+        case 1: launch_ocv_paths_l<1, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 2: launch_ocv_paths_l<2, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 4: launch_ocv_paths_l<4, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 8: launch_ocv_paths_l<8, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 16: launch_ocv_paths_l<16, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        default: launch_ocv_paths_l<32, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        }
     }
     return hipGetLastError();
 }
