@@ -205,9 +205,12 @@ __device__ __forceinline__ void p16_relative(const uint32_t (&Labs)[DPL / 2], ui
 #pragma unroll
     for (int i = 1; i < M; i += 2) mn = (i + 1 < M) ? pk_min3_p(mn, Labs[i], Labs[i + 1]) : pk_min(mn, Labs[i]);
     mn = line_min_u32<LPL>(pk_min(mn, alignbit16(mn, mn)));   // (min, min) in every lane of the line
-    const uint32_t off = mn - kBaseP2;                    // pattern(L) - off = pattern(L - min)
+    uint32_t off = mn - kBaseP2;                          // pattern(L) - off = pattern(L - min)
+    asm("" : "+v"(off));                                  // keep (Labs - off): not (Labs - mn) + kBase
+    // A plain 32-bit subtract is the packed one here (no borrow crosses the halves: every
+    // half of Labs is >= min >= kBase), and v_sub_u32 issues at twice v_pk_sub_u16's rate.
 #pragma unroll
-    for (int i = 0; i < M; i++) Lr[i] = pk_sub(Labs[i], off);
+    for (int i = 0; i < M; i++) Lr[i] = Labs[i] - off;
 }
 
 // One recurrence step of the lane's pairs, costs computed on the fly:
@@ -226,7 +229,7 @@ __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F
     constexpr int SH = LPL == 16 ? 1 : 2;
     uint32_t q[M];
 #pragma unroll
-    for (int i = 0; i < M; i++) q[i] = pk_add(Lr[i], P1P1);
+    for (int i = 0; i < M; i++) q[i] = Lr[i] + P1P1;      // = pk_add: halves <= kInfP | kBaseP, no carry
     const uint32_t X = row_shr_n<SH>(q[M - 1], kInfP2);   // previous lane: its .hi is q(d0 - 1)
     const uint32_t Y = row_shl_n<SH>(q[0], kInfP2);       // next lane: its .lo is q(d0 + DPL)
     uint32_t Oprev = alignbit16(q[0], X);                 // (q(d-1), q(d)) for pair 0
@@ -730,7 +733,7 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
         const uint32_t TT = (uint32_t)T * 0x10001u;
         uint32_t acc = 0;
 #pragma unroll
-        for (int j = 0; j < NWD; j++) acc = pk_add(acc, pk_add(pk_subs(TT, E[j]), pk_subs(TT, O[j])));
+        for (int j = 0; j < NWD; j++) acc += pk_subs(TT, E[j]) + pk_subs(TT, O[j]);   // halves <= 2 * NWD * 2041: no carry
         const int tot = (int)row_sum_u32(__builtin_amdgcn_sad_u16(acc, 0u, 0u));
         const int win = max(T - minS, 0) + (best > 0 ? max(T - sm, 0) : 0) + (best < g.D - 1 ? max(T - sp, 0) : 0);
         int outside = tot - win;
