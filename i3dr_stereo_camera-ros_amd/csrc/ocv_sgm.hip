@@ -151,12 +151,23 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         if (d >= g.D) { d -= g.D; k++; }
     }
     __syncthreads();
+    // horizontal box: thread (segment, d) slides its window over the segment's outputs
+    // (2 LDS reads per output after the first; int sums, so any order is exact)
     const int nout = min(kPixXB, g.width1 - x0);
     int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D;     // the block's outputs are contiguous
-    for (int i = tid; i < nout * g.D; i += 256) {
+    const int nseg = max(256 / g.D, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
+    for (int t = tid; t < nseg * g.D; t += 256) {
+        const int seg = t / g.D, dd = t - seg * g.D;
+        const int xa = seg * seglen, xb = min(xa + seglen, nout);
+        if (xa >= xb) continue;
+        const int16_t* Pd = P + dd;
         int sum = 0;
-        for (int t = 0; t <= 2 * SW2; t++) sum += P[i + t * g.D];   // P[(xo + t) * D + d], i = xo * D + d
-        dst[i] = (int16_t)sum;
+        for (int u = 0; u <= BW; u++) sum += Pd[(xa + u) * g.D];
+        dst[xa * g.D + dd] = (int16_t)sum;
+        for (int xo = xa + 1; xo < xb; xo++) {
+            sum += Pd[(xo + BW) * g.D] - Pd[(xo - 1) * g.D];
+            dst[xo * g.D + dd] = (int16_t)sum;
+        }
     }
 }
 

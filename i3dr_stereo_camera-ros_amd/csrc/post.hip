@@ -108,6 +108,7 @@ __global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d,
                                                   int newVal, int maxDiff, int* __restrict__ lab, int* __restrict__ cnt)
 {
     __shared__ int l[kSpkTW * kSpkTH];
+    __shared__ int lcnt[kSpkTW * kSpkTH];
     __shared__ int16_t v[kSpkTW * kSpkTH];
     const int x0 = blockIdx.x * kSpkTW, y0 = blockIdx.y * kSpkTH;
     for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d,
         const int dv = (x < W && y < H) ? d[(size_t)y * stride + x] : newVal;
         v[i] = (int16_t)dv;
         l[i] = dv != newVal ? i : -1;
+        lcnt[i] = 0;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
@@ -125,59 +127,72 @@ __global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d,
         if (ty + 1 < kSpkTH) { const int q = v[i + kSpkTW]; if (q != newVal && abs(a - q) <= maxDiff) luf_union(l, i, i + kSpkTW); }
     }
     __syncthreads();
+    // tile-local roots and component sizes (LDS atomics); each local root's pixel carries its
+    // tile size in cnt, every other pixel 0
+    for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
+        const int x = x0 + (i & (kSpkTW - 1)), y = y0 + i / kSpkTW;
+        if (l[i] < 0 || x >= W || y >= H) continue;
+        int r = i;
+        while (l[r] != r) r = l[r];
+        atomicAdd(&lcnt[r], 1);
+        lab[y * W + x] = (y0 + r / kSpkTW) * W + x0 + (r & (kSpkTW - 1));
+    }
+    __syncthreads();
     for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
         const int x = x0 + (i & (kSpkTW - 1)), y = y0 + i / kSpkTW;
         if (x >= W || y >= H) continue;
-        int r = -1;
-        if (l[i] >= 0) {
-            r = i;
-            while (l[r] != r) r = l[r];
-            r = (y0 + r / kSpkTW) * W + x0 + (r & (kSpkTW - 1));
-        }
-        lab[y * W + x] = r;
-        cnt[y * W + x] = 0;
+        if (l[i] < 0) lab[y * W + x] = -1;
+        cnt[y * W + x] = l[i] == i ? lcnt[i] : 0;
     }
 }
 
 // Phase 2: the edges that cross tile borders (right column and bottom row of each tile),
-// merged with the global union-find.
+// merged with the global union-find. Along a border, consecutive edges mostly join the
+// same pair of tile-local components: an edge whose (label, label) pair equals the previous
+// edge's is already covered by that edge's union (labels are read before any union of this
+// block; any label read is a valid ancestor, so equal pairs mean the same two sets).
 __global__ __launch_bounds__(256) void k_spk_border(const int16_t* __restrict__ d, size_t stride, int W, int H,
                                                     int newVal, int maxDiff, int* __restrict__ lab)
 {
+    __shared__ int pa[kSpkTH + kSpkTW], pb[kSpkTH + kSpkTW];
     const int x0 = blockIdx.x * kSpkTW, y0 = blockIdx.y * kSpkTH;
     const int t = threadIdx.x;
-    int x, y, dx, dy;
-    if (t < kSpkTH) { x = x0 + kSpkTW - 1; y = y0 + t; dx = 1; dy = 0; }             // right edge
-    else if (t < kSpkTH + kSpkTW) { x = x0 + t - kSpkTH; y = y0 + kSpkTH - 1; dx = 0; dy = 1; }  // bottom edge
-    else return;
-    if (x + dx >= W || y + dy >= H || x >= W || y >= H) return;
-    const int a = d[(size_t)y * stride + x], q = d[(size_t)(y + dy) * stride + x + dx];
-    if (a != newVal && q != newVal && abs(a - q) <= maxDiff) uf_union(lab, y * W + x, (y + dy) * W + x + dx);
+    constexpr int NE = kSpkTH + kSpkTW;
+    int x = 0, y = 0, dx = 0, dy = 0;
+    bool e = false;
+    if (t < kSpkTH) { x = x0 + kSpkTW - 1; y = y0 + t; dx = 1; }                   // right edge
+    else if (t < NE) { x = x0 + t - kSpkTH; y = y0 + kSpkTH - 1; dy = 1; }          // bottom edge
+    if (t < NE && x + dx < W && y + dy < H && x < W && y < H) {
+        const int a = d[(size_t)y * stride + x], q = d[(size_t)(y + dy) * stride + x + dx];
+        e = a != newVal && q != newVal && abs(a - q) <= maxDiff;
+    }
+    if (t < NE) {
+        pa[t] = e ? lab[y * W + x] : -1;
+        pb[t] = e ? lab[(y + dy) * W + x + dx] : -1;
+    }
+    __syncthreads();
+    if (!e) return;
+    if (t != 0 && t != kSpkTH && pa[t - 1] == pa[t] && pb[t - 1] == pb[t]) return;
+    uf_union(lab, y * W + x, (y + dy) * W + x + dx);
 }
 
-// After the union phase (a kernel boundary away): every label points straight at its root.
-// Concurrent rewrites only ever replace a label by one of its ancestors, so the chains other
-// threads are walking stay valid.
-__global__ __launch_bounds__(256) void k_spk_flatten(int W, int H, int* __restrict__ lab)
+// After the union phase (a kernel boundary away): every label is pointed straight at its
+// root (concurrent rewrites only ever replace a label by one of its ancestors, so the chains
+// other threads are walking stay valid), and each tile-local root that is not the global
+// root adds its tile size (k_spk_tile) to the global root's counter: one atomic per
+// tile-local component, not per pixel. Only "size <= maxSize" is ever asked, so a counter
+// already past maxSize takes no more adds (a count stays exact while it is <= maxSize).
+__global__ __launch_bounds__(256) void k_spk_count(int W, int H, int maxSize, int* __restrict__ lab,
+                                                   int* __restrict__ cnt)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H || lab[i] < 0) return;
-    lab[i] = uf_root(lab, i);
-}
-
-// Component sizes: the lanes of a wave that share a root add once (one atomic per distinct
-// root per wave instead of one per pixel: a large region is otherwise a single hot counter).
-__global__ __launch_bounds__(256) void k_spk_count(int W, int H, const int* __restrict__ lab, int* __restrict__ cnt)
-{
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int root = i < W * H ? lab[i] : -1;
-    uint64_t todo = __ballot(root >= 0);
-    while (todo) {
-        const int leader = __builtin_amdgcn_readlane(root, __builtin_ctzll(todo));
-        const uint64_t same = __ballot(root == leader) & todo;
-        if ((threadIdx.x & 63) == __builtin_ctzll(same)) atomicAdd(&cnt[leader], __builtin_popcountll(same));
-        todo &= ~same;
-    }
+    const int root = uf_root(lab, i);
+    lab[i] = root;
+    const int own = cnt[i];                        // > 0: i is a tile-local root
+    if (own > 0 && root != i &&
+        __hip_atomic_load(&cnt[root], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= maxSize)
+        atomicAdd(&cnt[root], own);
 }
 
 __global__ __launch_bounds__(256) void k_spk_apply(int16_t* __restrict__ d, size_t stride, int W, int H, int newVal,
@@ -201,8 +216,7 @@ hipError_t launch_speckle(int16_t* d, size_t stride, int W, int H, int newVal, i
     const dim3 tiles((W + kSpkTW - 1) / kSpkTW, (H + kSpkTH - 1) / kSpkTH);
     hipLaunchKernelGGL(k_spk_tile, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab, cnt);
     hipLaunchKernelGGL(k_spk_border, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
-    hipLaunchKernelGGL(k_spk_flatten, grid, block, 0, st, W, H, lab);
-    hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, lab, cnt);
+    hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, maxSize, lab, cnt);
     hipLaunchKernelGGL(k_spk_apply, grid, block, 0, st, d, stride, W, H, newVal, maxSize, lab, cnt);
     return hipGetLastError();
 }

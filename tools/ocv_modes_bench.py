@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--cpu", action="store_true", help="also time the CPU restatement (1 thread)")
+    ap.add_argument("--case", default="", help="run only the cases whose name contains this")
     a = ap.parse_args()
     import torch
     pkg = ge.load_package()
@@ -38,6 +39,8 @@ def main():
     eng = pkg.Engine(0)
     st = torch.cuda.Stream()
     for name, h, w, mode, kw in cases:
+        if a.case not in name:
+            continue
         p = pkg.default_params(mode, **kw)
         eng.set_params(p)
         left, right, _ = synth.stereo_pair(h, w, max(p.min_disparity, 0), p.num_disparities, seed=3)
