@@ -343,12 +343,16 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     int nmax = 0;
 #pragma unroll
     for (int w = 0; w < NLW; w++) nmax = max(nmax, __builtin_amdgcn_readlane(n, w * LPL));
-    // cell offset of step i (clamped to the line) = base + i * step, branch-free
+    // cell offset of step i (clamped to the line) = base + min(i, ilast) * step. LPL 32 (the
+    // latency-bound small frames) advances two running offsets by a select + 64-bit add per
+    // step (no quarter-rate multiplies in the step chain: C1 paths 122 -> 115 us); LPL 16
+    // recomputes them, which keeps 6 waves/SIMD (76 VGPRs instead of 83) where lines fill the
+    // SIMDs.
     const int ybase = ry >= 0 ? s0 : g.H - 1 - s0;
     const long long cbase = ((long long)ybase * g.width1 + x0) * g.D;
     const long long cstep = ((long long)ry * g.width1 + rx) * g.D;
     const int ilast = max(n - 1, 0);
-    auto cell = [&](int i) -> size_t { return (size_t)(cbase + (long long)min(i, ilast) * cstep); };
+    auto cell = [&](int i) -> long long { return cbase + (long long)min(i, ilast) * cstep; };
     int Lp[DPL], mLp = 0;
     bool pv = false;
 #pragma unroll
@@ -360,9 +364,9 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     int Cb[PF][DPL];
     const bool lane_act = p * DPL < g.D;
     const int dl = min(p * DPL, g.D - DPL);
-    auto load = [&](int (&c)[DPL], int i) {
+    auto load = [&](int (&c)[DPL], long long off) {
         int16_t v[DPL];
-        load_i16<DPL>(C + cell(i) + dl, v);
+        load_i16<DPL>(C + off + dl, v);
 #pragma unroll
         for (int k = 0; k < DPL; k++) c[k] = lane_act ? (int)v[k] : 0;
     };
@@ -371,7 +375,8 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // volumes (vols + trash_off).
     int16_t* const tr = vols + trash_off + lane * DPL;
 #pragma unroll
-    for (int q = 0; q < PF; q++) load(Cb[q], q);
+    for (int q = 0; q < PF; q++) load(Cb[q], cell(q));
+    long long st_off = cbase, ld_off = cell(PF);       // cell(i), cell(i + PF)
     for (int i0 = 0; i0 < nmax; i0 += PF) {
 #pragma unroll
         for (int q = 0; q < PF; q++) {
@@ -379,13 +384,18 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             int L[DPL];
             const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, pv, p, g, L);
             const bool ok = lane_act && i < n;
-            const size_t o = cell(i) + dl;
-            store_i16<DPL>((int16_t*)((uintptr_t)(V + o) * ok + (uintptr_t)tr * !ok), L);
+            if constexpr (LPL != 32) st_off = cell(i);
+            store_i16<DPL>(ok ? V + st_off + dl : tr, L);
             mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
             for (int k = 0; k < DPL; k++) Lp[k] = L[k];
             pv = true;
-            load(Cb[q], i + PF);
+            if constexpr (LPL != 32) ld_off = cell(i + PF);
+            load(Cb[q], ld_off);
+            if constexpr (LPL == 32) {
+                st_off += i < ilast ? cstep : 0;
+                ld_off += i + PF < ilast ? cstep : 0;
+            }
         }
     }
 }
