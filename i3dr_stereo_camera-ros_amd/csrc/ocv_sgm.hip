@@ -247,6 +247,52 @@ __device__ __forceinline__ void store_i16(int16_t* p, const int (&v)[DPL])
     }
 }
 
+// The same through a raw buffer descriptor (32-bit byte offsets; an offset past the
+// descriptor's range reads 0 / drops the store: the 32-lane path kernel's masking)
+template <int DPL>
+__device__ __forceinline__ void bload_i16(__amdgpu_buffer_rsrc_t rs, uint32_t off, int (&v)[DPL])
+{
+    if constexpr (DPL == 1) {
+        v[0] = (int)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0);
+        return;
+    }
+    uint32_t w[DPL / 2 > 0 ? DPL / 2 : 1];
+    if constexpr (DPL == 2) w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+    else if constexpr (DPL == 4) { const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0); w[0] = t[0]; w[1] = t[1]; }
+    else {
+#pragma unroll
+        for (int c = 0; c < DPL / 8; c++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * c, 0, 0);
+            w[4 * c] = t[0]; w[4 * c + 1] = t[1]; w[4 * c + 2] = t[2]; w[4 * c + 3] = t[3];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < DPL / 2; i++) { v[2 * i] = (int)(int16_t)w[i]; v[2 * i + 1] = (int)w[i] >> 16; }
+}
+template <int DPL>
+__device__ __forceinline__ void bstore_i16(__amdgpu_buffer_rsrc_t rs, uint32_t off, const int (&v)[DPL])
+{
+    constexpr int aux = 2;                               // nt: streamed once into the WTA
+    if constexpr (DPL == 1) {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[0], rs, off, 0, aux);
+        return;
+    }
+    uint32_t w[DPL / 2 > 0 ? DPL / 2 : 1];
+#pragma unroll
+    for (int i = 0; i < DPL / 2; i++) w[i] = ((uint32_t)v[2 * i] & 0xFFFFu) | ((uint32_t)v[2 * i + 1] << 16);
+    if constexpr (DPL == 2) __builtin_amdgcn_raw_buffer_store_b32(w[0], rs, off, 0, aux);
+    else if constexpr (DPL == 4) {
+        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, rs, off, 0, aux);
+    } else {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int c = 0; c < DPL / 8; c++)
+            __builtin_amdgcn_raw_buffer_store_b128((v4u){w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]}, rs,
+                                                   off + 16 * c, 0, aux);
+    }
+}
+
 // OpenCV recurrence of one cell with int16 storage semantics, for a path line held by LPL
 // lanes (16: one row of the wave; 32: two rows) — lane p: d = p*DPL .. p*DPL + DPL - 1.
 // Entries with d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
@@ -312,7 +358,7 @@ __device__ __forceinline__ int line_min_i32(int v)
 template <int DPL, int LPL>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, int16_t* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
-                                                  int4 nblk1)
+                                                  int4 nblk1, int use_buf)
 {
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
     // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
@@ -343,60 +389,83 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     int nmax = 0;
 #pragma unroll
     for (int w = 0; w < NLW; w++) nmax = max(nmax, __builtin_amdgcn_readlane(n, w * LPL));
-    // cell offset of step i (clamped to the line) = base + min(i, ilast) * step. LPL 32 (the
-    // latency-bound small frames) advances two running offsets by a select + 64-bit add per
-    // step (no quarter-rate multiplies in the step chain: C1 paths 122 -> 115 us); LPL 16
-    // recomputes them, which keeps 6 waves/SIMD (76 VGPRs instead of 83) where lines fill the
-    // SIMDs.
+    // cell offset of step i = base + i * step (clamped to the line for LPL 16)
     const int ybase = ry >= 0 ? s0 : g.H - 1 - s0;
     const long long cbase = ((long long)ybase * g.width1 + x0) * g.D;
     const long long cstep = ((long long)ry * g.width1 + rx) * g.D;
     const int ilast = max(n - 1, 0);
     auto cell = [&](int i) -> long long { return cbase + (long long)min(i, ilast) * cstep; };
     int Lp[DPL], mLp = 0;
-    bool pv = false;
 #pragma unroll
     for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
     // C of the next PF steps in flight (one global-load latency per PF steps, not per step);
-    // one vector load per lane (lanes past D read the last valid group and drop it): no
-    // exec-masked branch around the loads, so the prefetch keeps counted waits
+    // one vector load per lane (lanes past D read the last valid group: their C never
+    // reaches an entry with d < D): no exec-masked branch around the loads, so the prefetch
+    // keeps counted waits
     constexpr int PF = DPL <= 4 ? SGM_OCV_PF : 4;
     int Cb[PF][DPL];
     const bool lane_act = p * DPL < g.D;
     const int dl = min(p * DPL, g.D - DPL);
-    auto load = [&](int (&c)[DPL], long long off) {
-        int16_t v[DPL];
-        load_i16<DPL>(C + off + dl, v);
+    // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop).
+    // The first PF steps are peeled (pv = false only at step 0, a constant elsewhere).
+    if (use_buf) {
+        // Volumes < 2 GB: raw buffer loads and stores with 32-bit byte offsets that just move
+        // by the step; a step past the line's end reads whatever lies there (unused) or 0 past
+        // the range, and a store that must not land is sent past the range, where the hardware
+        // drops it. No clamps, 64-bit address selects or trash slot in the step chain (C1
+        // paths 115 -> 90 us: a small frame's line is issue-bound, 61 -> 48 instructions/step).
+        const uint32_t nbytes = (uint32_t)((size_t)g.width1 * g.H * g.D * 2);
+        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)nbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)nbytes, 0x00020000);
+        const uint32_t bstep = (uint32_t)(cstep * 2);
+        uint32_t st_b = (uint32_t)((cbase + dl) * 2), ld_b = st_b;
 #pragma unroll
-        for (int k = 0; k < DPL; k++) c[k] = lane_act ? (int)v[k] : 0;
-    };
-    // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop):
-    // steps past a line's end and lanes past D store to a per-lane trash slot after the
-    // volumes (vols + trash_off).
-    int16_t* const tr = vols + trash_off + lane * DPL;
+        for (int q = 0; q < PF; q++) { bload_i16<DPL>(rsC, ld_b, Cb[q]); ld_b += bstep; }
+        auto steps = [&](int i0, auto first) {
 #pragma unroll
-    for (int q = 0; q < PF; q++) load(Cb[q], cell(q));
-    long long st_off = cbase, ld_off = cell(PF);       // cell(i), cell(i + PF)
-    for (int i0 = 0; i0 < nmax; i0 += PF) {
+            for (int q = 0; q < PF; q++) {
+                const int i = i0 + q;
+                int L[DPL];
+                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L);
+                bstore_i16<DPL>(rsV, lane_act && i < n ? st_b : 0x80000000u, L);
+                mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
-        for (int q = 0; q < PF; q++) {
-            const int i = i0 + q;
-            int L[DPL];
-            const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, pv, p, g, L);
-            const bool ok = lane_act && i < n;
-            if constexpr (LPL != 32) st_off = cell(i);
-            store_i16<DPL>(ok ? V + st_off + dl : tr, L);
-            mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
-#pragma unroll
-            for (int k = 0; k < DPL; k++) Lp[k] = L[k];
-            pv = true;
-            if constexpr (LPL != 32) ld_off = cell(i + PF);
-            load(Cb[q], ld_off);
-            if constexpr (LPL == 32) {
-                st_off += i < ilast ? cstep : 0;
-                ld_off += i + PF < ilast ? cstep : 0;
+                for (int k = 0; k < DPL; k++) Lp[k] = L[k];
+                bload_i16<DPL>(rsC, ld_b, Cb[q]);
+                st_b += bstep;
+                ld_b += bstep;
             }
-        }
+        };
+        if (nmax > 0) steps(0, std::true_type{});
+        for (int i0 = PF; i0 < nmax; i0 += PF) steps(i0, std::false_type{});
+    } else {
+        // larger volumes: 64-bit addresses, clamped to the line; steps past a line's end and
+        // lanes past D store to a per-lane trash slot after the volumes (vols + trash_off)
+        int16_t* const tr = vols + trash_off + lane * DPL;
+        auto load = [&](int (&c)[DPL], long long off) {
+            int16_t v[DPL];
+            load_i16<DPL>(C + off + dl, v);
+#pragma unroll
+            for (int k = 0; k < DPL; k++) c[k] = v[k];
+        };
+#pragma unroll
+        for (int q = 0; q < PF; q++) load(Cb[q], cell(q));
+        auto steps = [&](int i0, auto first) {
+#pragma unroll
+            for (int q = 0; q < PF; q++) {
+                const int i = i0 + q;
+                int L[DPL];
+                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L);
+                const bool ok = lane_act && i < n;
+                store_i16<DPL>(ok ? V + cell(i) + dl : tr, L);
+                mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
+#pragma unroll
+                for (int k = 0; k < DPL; k++) Lp[k] = L[k];
+                load(Cb[q], cell(i + PF));
+            }
+        };
+        if (nmax > 0) steps(0, std::true_type{});
+        for (int i0 = PF; i0 < nmax; i0 += PF) steps(i0, std::false_type{});
     }
 }
 
@@ -513,8 +582,10 @@ static void launch_ocv_paths_l(const int16_t* C, int16_t* vols, size_t vol_elems
         total += nb[i];
     }
     const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
+    // 32-bit buffer offsets when a volume is < 2 GB (SGM_OCV_NO_BUF=1 forces the 64-bit path)
+    const int use_buf = (size_t)g.width1 * g.H * g.D * 2 < 0x7FFFFFFFu && !getenv("SGM_OCV_NO_BUF");
     hipLaunchKernelGGL((k_ocv_paths<DPL, LPL>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
-                       dirmask, a, b);
+                       dirmask, a, b, use_buf);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by

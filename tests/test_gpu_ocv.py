@@ -64,12 +64,17 @@ def test_ocv_node_defaults_c1(engine, oracle, synth, pkg, mode):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("nobuf", ["", "1"], ids=["buf32", "ptr64"])
 @pytest.mark.parametrize("lanes", ["16", "32"])
 @pytest.mark.parametrize("mode,h,w,minD,D,block", [(0, 480, 640, 9, 64, 15), (1, 96, 500, 0, 128, 5),
                                                    (0, 40, 600, -4, 256, 7), (1, 33, 200, 3, 48, 3)])
-def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, lanes, mode, h, w, minD, D, block):
-    """Both path-kernel shapes (16 and 32 lanes per line, SGM_OCV_LPL) on the same inputs."""
+def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf, lanes, mode, h, w, minD, D, block):
+    """Both path-kernel shapes (16 and 32 lanes per line, SGM_OCV_LPL) and both addressing
+    schemes (32-bit buffer offsets; the 64-bit clamped pointers of > 2 GB volumes,
+    SGM_OCV_NO_BUF) on the same inputs."""
     monkeypatch.setenv("SGM_OCV_LPL", lanes)
+    if nobuf:
+        monkeypatch.setenv("SGM_OCV_NO_BUF", nobuf)
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h + D)
     p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block)
     engine.set_params(p)
