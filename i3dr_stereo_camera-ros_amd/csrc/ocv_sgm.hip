@@ -192,15 +192,31 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
     const bool tail = y1 - 1 >= 1 && y1 - 1 + SH2 >= H;    // the segment reaches the repeated rows
     const int rep = fullDP ? g.P2 : g.P2 + (tail ? window(ylast) : 0);
     int s = window(y0);
-    for (int y = y0; y < y1; y++) {
-        int v;
-        if (y == 0 || y + SH2 < H) {
-            if (y > y0) s += hs[(size_t)(y + SH2) * rs + i] - hs[(size_t)max(y - SH2 - 1, 0) * rs + i];
-            v = g.P2 + s;
-        } else {
-            v = rep;
+    // rows in chunks of 8: the chunk's 16 entering / leaving rows are loaded together (clamped
+    // rows, used only where the window slides), so a thread keeps 16 loads in flight instead
+    // of one dependent pair per row (C1: 30 -> 24 us)
+    constexpr int U = 8;
+    for (int yb = y0; yb < y1; yb += U) {
+        int ha[U], hb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int y = min(yb + u, y1 - 1);
+            ha[u] = hs[(size_t)min(y + SH2, H - 1) * rs + i];
+            hb[u] = hs[(size_t)max(y - SH2 - 1, 0) * rs + i];
         }
-        C[(size_t)y * rs + i] = (int16_t)v;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int y = yb + u;
+            if (y >= y1) break;                            // uniform over the block
+            int v;
+            if (y == 0 || y + SH2 < H) {
+                if (y > y0) s += ha[u] - hb[u];
+                v = g.P2 + s;
+            } else {
+                v = rep;
+            }
+            C[(size_t)y * rs + i] = (int16_t)v;
+        }
     }
 }
 
