@@ -111,8 +111,11 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
     const int NR = NX + g.D - 1;                           // right-image BT entries needed
     const size_t plane = (size_t)g.W * g.H;
     int16_t* P = (int16_t*)lds_pix;                        // [NX][D]
-    uint8_t* bl = lds_pix + (size_t)2 * NX * g.D;          // left  (u, lo, hi) x 2 channels x NX
-    uint8_t* br = bl + 6 * NX;                             // right (v, lo, hi) x 2 channels x NR
+    // BT intervals as 8-byte records (u, lo, hi of channel 0, then of channel 1, 2 pad):
+    // a cell's six reads per side share one address (immediate offsets), which matters
+    // because this kernel is VALU-bound (one address add per read otherwise)
+    uint8_t* bl = lds_pix + (((size_t)2 * NX * g.D + 7) & ~(size_t)7);   // left  [NX] records
+    uint8_t* br = bl + 8 * NX;                                           // right [NR] records
     // staged column i -> x1 = clamp(x0 - SW2 + i); right entry r -> xr = xlo - minD - (D-1) + r
     const int xlo = g.minX1 + min(max(x0 - SW2, 0), g.width1 - 1);
     for (int i = tid; i < 2 * NX; i += 256) {
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
         int u, lo, hi;
         bt_lohi(planes + c * plane + (size_t)y * g.W, x, g.W, u, lo, hi);
-        bl[(c * 3 + 0) * NX + k] = (uint8_t)u; bl[(c * 3 + 1) * NX + k] = (uint8_t)lo; bl[(c * 3 + 2) * NX + k] = (uint8_t)hi;
+        bl[8 * k + 3 * c] = (uint8_t)u; bl[8 * k + 3 * c + 1] = (uint8_t)lo; bl[8 * k + 3 * c + 2] = (uint8_t)hi;
     }
     const int xr0 = xlo - g.minD - (g.D - 1);
     for (int i = tid; i < 2 * NR; i += 256) {
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         const int xr = min(max(xr0 + r, 0), g.W - 1);
         int v, lo, hi;
         bt_lohi(planes + (2 + c) * plane + (size_t)y * g.W, xr, g.W, v, lo, hi);
-        br[(c * 3 + 0) * NR + r] = (uint8_t)v; br[(c * 3 + 1) * NR + r] = (uint8_t)lo; br[(c * 3 + 2) * NR + r] = (uint8_t)hi;
+        br[8 * r + 3 * c] = (uint8_t)v; br[8 * r + 3 * c + 1] = (uint8_t)lo; br[8 * r + 3 * c + 2] = (uint8_t)hi;
     }
     __syncthreads();
     // (k, d) of flat index i = k * D + d, advanced by 256 per iteration without divisions
@@ -136,12 +139,13 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
     int k = tid / g.D, d = tid - k * g.D;
     for (int i = tid; i < NX * g.D; i += 256) {
         const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
-        const int r = x - g.minD - d - xr0;                // index of xr = x - minD - d
+        const uint8_t* L8 = bl + 8 * k;
+        const uint8_t* R8 = br + 8 * (x - g.minD - d - xr0);   // entry of xr = x - minD - d
         int acc = 0;
 #pragma unroll
         for (int c = 0; c < 2; c++) {
-            const int u = bl[(c * 3) * NX + k], ulo = bl[(c * 3 + 1) * NX + k], uhi = bl[(c * 3 + 2) * NX + k];
-            const int v = br[(c * 3) * NR + r], v0 = br[(c * 3 + 1) * NR + r], v1 = br[(c * 3 + 2) * NR + r];
+            const int u = L8[3 * c], ulo = L8[3 * c + 1], uhi = L8[3 * c + 2];
+            const int v = R8[3 * c], v0 = R8[3 * c + 1], v1 = R8[3 * c + 2];
             const int c0 = max(0, max(u - v1, v0 - u));
             const int c1 = max(0, max(v - uhi, ulo - v));
             acc += min(c0, c1) >> (c == 0 ? 0 : 2);
@@ -568,7 +572,7 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes);
     const int NX = kPixXB + 2 * g.SW2;
-    const size_t lds = (size_t)2 * NX * g.D + 6 * NX + 6 * (NX + g.D - 1);
+    const size_t lds = (((size_t)2 * NX * g.D + 7) & ~(size_t)7) + 8 * NX + 8 * (NX + g.D - 1);
     if (lds <= 64 * 1024) {
         hipLaunchKernelGGL(k_ocv_pixhsum, dim3((g.width1 + kPixXB - 1) / kPixXB, g.H), dim3(256), lds, st, planes, g,
                            bufB);
