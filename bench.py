@@ -102,7 +102,48 @@ def cpu_baseline(cfg, budget_s=20.0):
     out["reference_path"] = {"value": 1.0 / dt1, "unit": "pairs/s", "cores": 1, "kind": "port",
                              "sample": f"1 frame {cfg['w']}x{cfg['h']} D={cfg['D']} OpenCV-StereoSGBM "
                                        f"MODE_SGBM restatement (block 5), single-threaded like OpenCV"}
+    out["c1_reference_matcher"] = c1_reference_matcher(orc, synth)
+    orc.set_threads(threads)
     return out
+
+
+def c1_reference_matcher(orc, synth, reps=20):
+    """BASELINE configs[0] (C1): the reference's own matcher at the generate_disparity node
+    defaults (640x480, minD 9, D 64, block 15, MODE_SGBM + medianBlur + filterSpeckles),
+    single-threaded CPU restatement beside the engine's bit-exact GPU restatement of it on the
+    same frame (device buffers, HIP events on the engine's stream). Reported beside the
+    census metric, never as `value`."""
+    import numpy as np
+    import torch
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    left, right, _ = synth.stereo_pair(480, 640, 9, 64, seed=1, with_truth=False)
+    p = pkg.default_params(pkg.MODE_OCV_SGBM5)
+    eng = pkg.Engine(torch.cuda.current_device(), p)
+    dl, dr = torch.from_numpy(left).cuda(), torch.from_numpy(right).cuda()
+    out = torch.empty((480, 640), dtype=torch.int16, device="cuda")
+    st = torch.cuda.Stream()
+    run = lambda: eng.match_device(dl.data_ptr(), dr.data_ptr(), 640, 480, 640, out.data_ptr(), 640, st.cuda_stream)
+    run()
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        run()
+    e1.record(st)
+    st.synchronize()
+    gpu_ms = e0.elapsed_time(e1) / reps
+    got = out.cpu().numpy()
+    eng.close()
+    op = orc.make_params(orc.MODE_OCV_SGBM5, **{k: v for k, v in p.as_dict().items() if k != "mode"})
+    orc.set_threads(1)
+    t0 = time.perf_counter()
+    ref = orc.match(op, left, right)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    return {"config": "C1 640x480 minD 9 D 64 block 15 MODE_SGBM + median + speckle (node defaults)",
+            "cpu_ms_per_frame": round(cpu_ms, 2), "cpu_cores": 1, "kind": "port",
+            "gpu_ms_per_frame": round(gpu_ms, 4), "gpu_pairs_per_s": round(1000.0 / gpu_ms, 1),
+            "bit_exact": bool(np.array_equal(got, ref))}
 
 
 def main():
