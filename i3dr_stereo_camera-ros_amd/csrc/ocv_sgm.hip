@@ -546,7 +546,10 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ v
             const int d = p * DPL + k;
             hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
         }
-        const bool rej = row_sum_u32(hit ? 1u : 0u) != 0u;
+        // every S saturated at MAX_COST: OpenCV's strict `Sval < minS` from minS = MAX_COST
+        // never fires, bestDisp stays -1 and the pixel ends up (minD - 1) * 16 = INVALID with
+        // no disp2 update, i.e. exactly a uniqueness reject
+        const bool rej = row_sum_u32(hit ? 1u : 0u) != 0u || minS >= 32767;
 #pragma unroll
         for (int k = 0; k < DPL; k++) srow[p * DPL + k] = (int16_t)S[k];
         const int sm = srow[max(best - 1, 0)], sp = srow[min(best + 1, g.D - 1)];

@@ -221,8 +221,10 @@ static void wta_pixel(const eff_t* e, int x, const int* Sp, int16_t* disp_row, w
         if (Sp[d] * (100 - e->uniq) < minS * 100 && abs(bestDisp - d) > 1) break;
     if (d < D) return;                         /* uniqueness reject: no disp2 update either */
     d = bestDisp;
+    /* bestDisp == -1 (every S saturated at MAX_COST) puts x2 one past the row; OpenCV reads
+     * a CostType there, which can never exceed minS == MAX_COST: no update */
     int x2 = x + e->minX1 - d - e->minD;
-    if (b->disp2cost[x2] > minS) { b->disp2cost[x2] = minS; b->disp2[x2] = (int16_t)(d + e->minD); }
+    if (d >= 0 && b->disp2cost[x2] > minS) { b->disp2cost[x2] = minS; b->disp2[x2] = (int16_t)(d + e->minD); }
     if (e->subpix && 0 < d && d < D - 1) {
         int denom2 = imax(Sp[d - 1] + Sp[d + 1] - 2 * Sp[d], 1);
         d = d * DISP_SCALE + ((Sp[d - 1] - Sp[d + 1]) * DISP_SCALE + denom2) / (denom2 * 2);

@@ -1,0 +1,106 @@
+"""GPU parity — seeded random configurations against the oracle, bit-exact.
+
+Each case draws a mode (census, MODE_SGBM, MODE_HH), an image size (including heights below
+the SAD window and widths that leave no valid column), a disparity window (negative minD
+included), penalties, uniqueness (0, ordinary, >= 100), LR / subpixel / median / speckle
+settings and an image kind (textured stereo pair, noise, or pairs with flat patches that
+trip the uniqueness and speckle rules). The seeds are fixed, so a failure names a
+reproducible configuration. Census cases also run through the pipelined device batch
+(`sgm_match_device_batch`) with a random frame count and through the exact row-band mode
+(`sgm_match_tiled_exact`) with a random band count.
+"""
+import numpy as np
+import pytest
+
+from conftest import to_oracle_params
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = 120
+
+
+def _images(rng, synth, h, w, minD, D, kind, seed):
+    if kind == "noise":
+        return (rng.integers(0, 256, (h, w), dtype=np.uint8), rng.integers(0, 256, (h, w), dtype=np.uint8))
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=seed, with_truth=False)
+    if kind == "flat":
+        left, right = left.copy(), right.copy()
+        for _ in range(int(rng.integers(1, 4))):
+            y0, x0 = int(rng.integers(0, h)), int(rng.integers(0, w))
+            hh, ww = int(rng.integers(1, h + 1)), int(rng.integers(1, w + 1))
+            v = int(rng.integers(0, 256))
+            left[y0:y0 + hh, x0:x0 + ww] = v
+            right[y0:y0 + hh, max(x0 - 3, 0):x0 + ww] = v
+    return left, right
+
+
+def _case(pkg, seed):
+    rng = np.random.default_rng(10_000 + seed)
+    mode = [pkg.MODE_CENSUS8, pkg.MODE_OCV_SGBM5, pkg.MODE_OCV_HH8][seed % 3]
+    D = int(rng.choice([16, 32, 48, 64, 80, 96, 128, 144, 256]))
+    minD = int(rng.integers(-12, 13))
+    span = max(D + minD, 0)
+    h = int(rng.choice([1, 2, 3, 7, 16, 23, 40]))
+    w = span + int(rng.integers(1, 90)) if rng.random() < 0.85 else int(rng.integers(1, span + 4))
+    kw = dict(num_disparities=D, min_disparity=minD,
+              uniqueness_ratio=int(rng.choice([0, 1, 5, 10, 15, 30, 99, 100, 120])),
+              disp12_max_diff=int(rng.choice([-1, 0, 1, 2, 5])),
+              speckle_window_size=int(rng.choice([0, 0, 10, 50])), speckle_range=int(rng.integers(1, 4)))
+    if mode == pkg.MODE_CENSUS8:
+        p1 = int(rng.integers(1, 40))
+        kw.update(p1=p1, p2=int(rng.integers(p1 + 1, 260)), subpixel=int(rng.integers(0, 2)),
+                  lr_check=int(rng.integers(0, 2)), median=int(rng.integers(0, 2)))
+    else:
+        p1 = int(rng.integers(1, 300))
+        kw.update(p1=p1, p2=int(rng.integers(p1 + 1, 1200)), block_size=int(rng.choice([1, 3, 5, 7, 9, 11, 15, 21])),
+                  prefilter_cap=int(rng.integers(1, 64)))
+    kind = str(rng.choice(["pair", "pair", "noise", "flat"]))
+    return rng, mode, h, w, kw, kind
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_fuzz_match(engine, oracle, synth, pkg, seed):
+    rng, mode, h, w, kw, kind = _case(pkg, seed)
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    left, right = _images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("seed", range(0, N_CASES, 3))        # the census cases
+def test_fuzz_device_batch(engine, oracle, synth, pkg, seed):
+    torch = pytest.importorskip("torch")
+    rng, mode, h, w, kw, kind = _case(pkg, seed)
+    assert mode == pkg.MODE_CENSUS8
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    n = int(rng.integers(1, 6))
+    frames = [_images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed + 97 * i)
+              for i in range(n)]
+    dl = [torch.from_numpy(f[0]).cuda() for f in frames]
+    dr = [torch.from_numpy(f[1]).cuda() for f in frames]
+    out = torch.full((n, h, w), 777, dtype=torch.int16, device="cuda")
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    engine.match_device_batch([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], w, h, w,
+                              [out[i].data_ptr() for i in range(n)], w, stream.cuda_stream)
+    stream.synchronize()
+    got = out.cpu().numpy()
+    op = to_oracle_params(oracle, p)
+    for i, (l, r) in enumerate(frames):
+        ref = oracle.match(op, l, r)
+        assert np.array_equal(got[i], ref), f"frame {i} of {n}, {h}x{w} {kw} {kind}: {(got[i] != ref).sum()} differ"
+
+
+@pytest.mark.parametrize("seed", range(0, N_CASES, 3))        # the census cases
+def test_fuzz_tiled_exact(engine, oracle, synth, pkg, seed):
+    rng, mode, h, w, kw, kind = _case(pkg, seed)
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    left, right = _images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed)
+    bands = int(rng.integers(1, min(h, 6) + 1))
+    got = engine.match_tiled_exact(left, right, bands)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{bands} bands, {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"

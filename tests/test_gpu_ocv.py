@@ -83,6 +83,23 @@ def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf,
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("uniq", [0, 10])
+def test_ocv_saturated_sums(engine, oracle, pkg, mode, uniq):
+    """Noise under a 21x21 box and a large P2 saturates S at MAX_COST for every d of some
+    pixels: OpenCV's strict `Sval < minS` from minS = MAX_COST then leaves bestDisp = -1, so
+    the pixel is INVALID whatever the uniqueness ratio (found by tests/test_gpu_fuzz.py)."""
+    rng = np.random.default_rng(56 + mode)
+    left = rng.integers(0, 256, (24, 200), dtype=np.uint8)
+    right = rng.integers(0, 256, (24, 200), dtype=np.uint8)
+    p = pkg.default_params(mode, min_disparity=-3, num_disparities=128, block_size=21, p1=128, p2=912,
+                           uniqueness_ratio=uniq, prefilter_cap=27, speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
 def test_ocv_small_images_bottom_rows(engine, oracle, pkg):
     """Heights below the SAD window (every row hits OpenCV's no-recompute rule)."""
     rng = np.random.default_rng(7)
