@@ -521,13 +521,22 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ v
     int16_t nxt[NDIR][DPL];
     load(min(w, nq - 1), nxt);
     for (int q = w; q < nq; q += 4) {
+        // S in OpenCV's order of saturating adds: pass 1 (dirs 0, 2, 3, 6: volume slots 0-3
+        // for MODE_SGBM, 0, 2, 3, 6 for MODE_HH) is added and saturated, then the fifth path
+        // (MODE_SGBM) or pass 2 (MODE_HH) — they differ once sums overflow int16
         int S[DPL];
 #pragma unroll
         for (int k = 0; k < DPL; k++) {
-            int s = 0;
-#pragma unroll
-            for (int v = 0; v < NDIR; v++) s += nxt[v][k];
-            S[k] = min(max(s, -32768), 32767);
+            int s1, s2;
+            if constexpr (NDIR == 5) {
+                s1 = nxt[0][k] + nxt[1][k] + nxt[2][k] + nxt[3][k];
+                s2 = nxt[4][k];
+            } else {
+                s1 = nxt[0][k] + nxt[2][k] + nxt[3][k] + nxt[6][k];
+                s2 = nxt[1][k] + nxt[4][k] + nxt[5][k] + nxt[7][k];
+            }
+            s1 = min(max(s1, -32768), 32767);
+            S[k] = min(max(s1 + s2, -32768), 32767);
         }
         load(min(q + 4, nq - 1), nxt);
         uint32_t km = 0xFFFFFFFFu;

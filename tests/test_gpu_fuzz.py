@@ -9,6 +9,8 @@ reproducible configuration. Census cases also run through the pipelined device b
 (`sgm_match_device_batch`) with a random frame count and through the exact row-band mode
 (`sgm_match_tiled_exact`) with a random band count.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -16,7 +18,7 @@ from conftest import to_oracle_params
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 120
+N_CASES = int(os.environ.get("SGM_FUZZ_CASES", "120"))   # a longer hunt: SGM_FUZZ_CASES=1000
 
 
 def _images(rng, synth, h, w, minD, D, kind, seed):
