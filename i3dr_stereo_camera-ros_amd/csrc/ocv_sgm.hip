@@ -313,6 +313,70 @@ __device__ __forceinline__ void bstore_i16(__amdgpu_buffer_rsrc_t rs, uint32_t o
     }
 }
 
+// Path volumes hold VT per cell: int16 (CostType, exact whenever no path cost can leave
+// int16) or int32 (Geom::wide: the cost volume itself may wrap, and OpenCV adds the int
+// path costs, not their CostType copies, into S). N dwords per lane for int32.
+template <int N>
+__device__ __forceinline__ void store_dw(uint32_t* p, const uint32_t (&w)[N])
+{
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (N == 1) __builtin_nontemporal_store(w[0], p);
+    else if constexpr (N == 2) __builtin_nontemporal_store((v2u){w[0], w[1]}, (v2u*)p);
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 4; c++)
+            __builtin_nontemporal_store((v4u){w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]}, (v4u*)p + c);
+    }
+}
+template <int N>
+__device__ __forceinline__ void bstore_dw(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t (&w)[N])
+{
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (N == 1) __builtin_amdgcn_raw_buffer_store_b32(w[0], rs, off, 0, 2);
+    else if constexpr (N == 2) __builtin_amdgcn_raw_buffer_store_b64((v2u){w[0], w[1]}, rs, off, 0, 2);
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 4; c++)
+            __builtin_amdgcn_raw_buffer_store_b128((v4u){w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]}, rs,
+                                                   off + 16 * c, 0, 2);
+    }
+}
+template <typename VT, int DPL>
+__device__ __forceinline__ void store_vals(VT* p, const int (&v)[DPL])
+{
+    if constexpr (sizeof(VT) == 2) store_i16<DPL>((int16_t*)p, v);
+    else store_dw<DPL>((uint32_t*)p, (const uint32_t (&)[DPL])v);
+}
+template <typename VT, int DPL>
+__device__ __forceinline__ void bstore_vals(__amdgpu_buffer_rsrc_t rs, uint32_t off, const int (&v)[DPL])
+{
+    if constexpr (sizeof(VT) == 2) bstore_i16<DPL>(rs, off, v);
+    else bstore_dw<DPL>(rs, off, (const uint32_t (&)[DPL])v);
+}
+template <typename VT, int DPL>
+__device__ __forceinline__ void load_vals(const VT* p, int (&v)[DPL])
+{
+    if constexpr (sizeof(VT) == 2) {
+        int16_t t[DPL];
+        load_i16<DPL>((const int16_t*)p, t);
+#pragma unroll
+        for (int k = 0; k < DPL; k++) v[k] = t[k];
+    } else if constexpr (DPL == 1) {
+        v[0] = *(const int*)p;
+    } else if constexpr (DPL == 2) {
+        const int2 t = *(const int2*)p;
+        v[0] = t.x; v[1] = t.y;
+    } else {
+#pragma unroll
+        for (int c = 0; c < DPL / 4; c++) {
+            const int4 t = ((const int4*)p)[c];
+            v[4 * c] = t.x; v[4 * c + 1] = t.y; v[4 * c + 2] = t.z; v[4 * c + 3] = t.w;
+        }
+    }
+}
+
 // OpenCV recurrence of one cell with int16 storage semantics, for a path line held by LPL
 // lanes (16: one row of the wave; 32: two rows) — lane p: d = p*DPL .. p*DPL + DPL - 1.
 // Entries with d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
@@ -330,9 +394,11 @@ __device__ __forceinline__ int line_shl1(int v, int p)
     const int t = __builtin_amdgcn_update_dpp(kMaxCost, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
     return p == LPL - 1 ? kMaxCost : t;
 }
+// Lout: the CostType (int16) path costs, the recurrence's state; Lraw: the int values
+// OpenCV adds into S (equal to Lout unless a cost left int16)
 template <int DPL, int LPL>
 __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DPL], int mLp, bool pv, int p,
-                                        const Geom& g, int (&Lout)[DPL])
+                                        const Geom& g, int (&Lout)[DPL], int (&Lraw)[DPL])
 {
     const int fromLeft = line_shr1<LPL>(Lp[DPL - 1], p);
     const int fromRight = line_shl1<LPL>(Lp[0], p);
@@ -348,6 +414,7 @@ __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DP
         if (!pv) { lm1 = d > 0 ? 0 : kMaxCost; lp1 = d < g.D - 1 ? 0 : kMaxCost; }
         const int v = Cp[k] + min(a, min(lm1 + g.P1, min(lp1 + g.P1, delta))) - delta;
         Lout[k] = d < g.D ? (int)(int16_t)v : kMaxCost;   // Lr is CostType (int16)
+        Lraw[k] = d < g.D ? v : kMaxCost;
         if (d < g.D) lmin = min(lmin, v);                  // minL over the int values
     }
     return lmin;
@@ -375,8 +442,8 @@ __device__ __forceinline__ int line_min_i32(int v)
 // line - width1 + 1. The lines of a block have (nearly) equal lengths; each stores only
 // while its own steps last. Fewer, wider lines (LPL 32) shorten each step's instruction
 // chain: a line is a sequential walk, and its step latency bounds the kernel.
-template <int DPL, int LPL>
-__global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, int16_t* __restrict__ vols,
+template <int DPL, int LPL, typename VT>
+__global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, VT* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
                                                   int4 nblk1, int use_buf)
 {
@@ -389,8 +456,9 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         b -= nb[i];
         slot++;
     }
-    int16_t* V = vols + (size_t)slot * vol_elems;
+    VT* V = vols + (size_t)slot * vol_elems;
     constexpr int NLW = 64 / LPL;                      // lines per wave
+    constexpr bool kRaw = sizeof(VT) == 4;             // store the int path costs (Geom::wide)
     const int lane = threadIdx.x, r = lane / LPL, p = lane % LPL;
     const int rx = dir_rx(dir), ry = dir_ry(dir);
     const int line = NLW * b + r;
@@ -434,25 +502,26 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         // the range, and a store that must not land is sent past the range, where the hardware
         // drops it. No clamps, 64-bit address selects or trash slot in the step chain (C1
         // paths 115 -> 90 us: a small frame's line is issue-bound, 61 -> 48 instructions/step).
-        const uint32_t nbytes = (uint32_t)((size_t)g.width1 * g.H * g.D * 2);
-        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)nbytes, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)nbytes, 0x00020000);
-        const uint32_t bstep = (uint32_t)(cstep * 2);
-        uint32_t st_b = (uint32_t)((cbase + dl) * 2), ld_b = st_b;
+        const size_t cells = (size_t)g.width1 * g.H * g.D;
+        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(cells * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsV =
+            __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)(cells * sizeof(VT)), 0x00020000);
+        const uint32_t bstep = (uint32_t)(cstep * 2), vstep = (uint32_t)(cstep * (long long)sizeof(VT));
+        uint32_t ld_b = (uint32_t)((cbase + dl) * 2), st_b = (uint32_t)((cbase + dl) * (long long)sizeof(VT));
 #pragma unroll
         for (int q = 0; q < PF; q++) { bload_i16<DPL>(rsC, ld_b, Cb[q]); ld_b += bstep; }
         auto steps = [&](int i0, auto first) {
 #pragma unroll
             for (int q = 0; q < PF; q++) {
                 const int i = i0 + q;
-                int L[DPL];
-                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L);
-                bstore_i16<DPL>(rsV, lane_act && i < n ? st_b : 0x80000000u, L);
+                int L[DPL], Lraw[DPL];
+                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
+                bstore_vals<VT, DPL>(rsV, lane_act && i < n ? st_b : 0x80000000u, kRaw ? Lraw : L);
                 mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];
                 bload_i16<DPL>(rsC, ld_b, Cb[q]);
-                st_b += bstep;
+                st_b += vstep;
                 ld_b += bstep;
             }
         };
@@ -461,7 +530,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     } else {
         // larger volumes: 64-bit addresses, clamped to the line; steps past a line's end and
         // lanes past D store to a per-lane trash slot after the volumes (vols + trash_off)
-        int16_t* const tr = vols + trash_off + lane * DPL;
+        VT* const tr = vols + trash_off + lane * DPL;
         auto load = [&](int (&c)[DPL], long long off) {
             int16_t v[DPL];
             load_i16<DPL>(C + off + dl, v);
@@ -474,10 +543,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
 #pragma unroll
             for (int q = 0; q < PF; q++) {
                 const int i = i0 + q;
-                int L[DPL];
-                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L);
+                int L[DPL], Lraw[DPL];
+                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
                 const bool ok = lane_act && i < n;
-                store_i16<DPL>(ok ? V + cell(i) + dl : tr, L);
+                store_vals<VT, DPL>(ok ? V + cell(i) + dl : tr, kRaw ? Lraw : L);
                 mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];
@@ -495,8 +564,8 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
 // (SURVEY Appendix A.6): S = saturate(sum of the NDIR L's); best = first minimal d through
 // one 16-lane min over (S + 32768) * 512 + d; uniqueness per element (S may be any int16
 // here); S[best +- 1] through a per-row LDS slice; then the shared disp2 / LR epilogue.
-template <int DPL, int NDIR>
-__global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ vols, size_t vol_elems, Geom g,
+template <int DPL, int NDIR, typename VT>
+__global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, size_t vol_elems, Geom g,
                                                    int16_t* __restrict__ out, size_t out_stride)
 {
     extern __shared__ uint32_t lds_ocv[];
@@ -513,12 +582,12 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const int16_t* __restrict__ v
     const size_t row0 = (size_t)y * g.width1 * g.D;
     // pixel 4q + r; the last group reads up to 3 pixels past the row (the next row or the
     // volume slack), results never stored
-    auto load = [&](int q, int16_t (&v)[NDIR][DPL]) {
-        const int16_t* base = vols + row0 + (size_t)(4 * q + r) * g.D + dl;
+    auto load = [&](int q, int (&v)[NDIR][DPL]) {
+        const VT* base = vols + row0 + (size_t)(4 * q + r) * g.D + dl;
 #pragma unroll
-        for (int k = 0; k < NDIR; k++) load_i16<DPL>(base + (size_t)k * vol_elems, v[k]);
+        for (int k = 0; k < NDIR; k++) load_vals<VT, DPL>(base + (size_t)k * vol_elems, v[k]);
     };
-    int16_t nxt[NDIR][DPL];
+    int nxt[NDIR][DPL];
     load(min(w, nq - 1), nxt);
     for (int q = w; q < nq; q += 4) {
         // S in OpenCV's order of saturating adds: pass 1 (dirs 0, 2, 3, 6: volume slots 0-3
@@ -597,11 +666,12 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
     return hipGetLastError();
 }
 
-// vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 int16 of trash slots
-template <int DPL, int LPL>
-static void launch_ocv_paths_l(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
+// vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 VT of trash slots
+template <int DPL, int LPL, typename VT>
+static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t vol_elems, const Geom& g, int dirmask,
                                hipStream_t st)
 {
+    VT* vols = (VT*)vols_;
     int ndir = 0;
     for (int i = 0; i < 8; i++) ndir += (dirmask >> i) & 1;
     const size_t trash_off = (size_t)ndir * vol_elems;
@@ -615,9 +685,17 @@ static void launch_ocv_paths_l(const int16_t* C, int16_t* vols, size_t vol_elems
     }
     const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
     // 32-bit buffer offsets when a volume is < 2 GB (SGM_OCV_NO_BUF=1 forces the 64-bit path)
-    const int use_buf = (size_t)g.width1 * g.H * g.D * 2 < 0x7FFFFFFFu && !getenv("SGM_OCV_NO_BUF");
-    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
+    const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < 0x7FFFFFFFu && !getenv("SGM_OCV_NO_BUF");
+    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf);
+}
+
+template <int DPL, int LPL>
+static void launch_ocv_paths_v(const int16_t* C, void* vols, size_t vol_elems, const Geom& g, int dirmask,
+                               hipStream_t st)
+{
+    if (g.wide) launch_ocv_paths_l<DPL, LPL, int32_t>(C, vols, vol_elems, g, dirmask, st);
+    else launch_ocv_paths_l<DPL, LPL, int16_t>(C, vols, vol_elems, g, dirmask, st);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
@@ -629,6 +707,7 @@ constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lane
 static int ocv_lanes_per_line(const Geom& g, int dirmask)
 {
     if (g.D <= 32) return 16;
+    if (g.D > 256 && g.D % 32 != 0) return 32;       // 16 lanes x DPL 32 would straddle D
     if (const char* e = getenv("SGM_OCV_LPL")) return atoi(e) == 32 ? 32 : 16;
     int waves = 0;
     for (int i = 0; i < 8; i++)
@@ -637,48 +716,58 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
     return waves < kOcvWideLineWaves ? 32 : 16;
 }
 
-hipError_t launch_ocv_paths(const int16_t* C, int16_t* vols, size_t vol_elems, const Geom& g, int dirmask,
+hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t vol_elems, const Geom& g, int dirmask,
                             hipStream_t st)
 {
     const int D = g.D;
     if (ocv_lanes_per_line(g, dirmask) == 32) {
-        if (D <= 64) launch_ocv_paths_l<2, 32>(C, vols, vol_elems, g, dirmask, st);
-        else if (D <= 128) launch_ocv_paths_l<4, 32>(C, vols, vol_elems, g, dirmask, st);
-        else if (D <= 256) launch_ocv_paths_l<8, 32>(C, vols, vol_elems, g, dirmask, st);
-        else launch_ocv_paths_l<16, 32>(C, vols, vol_elems, g, dirmask, st);
+        if (D <= 64) launch_ocv_paths_v<2, 32>(C, vols, vol_elems, g, dirmask, st);
+        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, vols, vol_elems, g, dirmask, st);
+        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, vols, vol_elems, g, dirmask, st);
+        else launch_ocv_paths_v<16, 32>(C, vols, vol_elems, g, dirmask, st);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_l<1, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 2: launch_ocv_paths_l<2, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 4: launch_ocv_paths_l<4, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 8: launch_ocv_paths_l<8, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 16: launch_ocv_paths_l<16, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        default: launch_ocv_paths_l<32, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 1: launch_ocv_paths_v<1, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 2: launch_ocv_paths_v<2, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 4: launch_ocv_paths_v<4, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 8: launch_ocv_paths_v<8, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 16: launch_ocv_paths_v<16, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        default: launch_ocv_paths_v<32, 16>(C, vols, vol_elems, g, dirmask, st); break;
         }
     }
     return hipGetLastError();
 }
 
-template <int DPL>
-static void launch_ocv_wta_dpl(const int16_t* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+template <int DPL, typename VT>
+static void launch_ocv_wta_dpl(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
                                size_t out_stride, hipStream_t st)
 {
     const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
+    const VT* v = (const VT*)vols;
     if (ndir == 8)
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8>), dim3(g.H), dim3(256), lds, st, vols, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
     else
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5>), dim3(g.H), dim3(256), lds, st, vols, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
 }
 
-hipError_t launch_ocv_wta(const int16_t* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
-                          size_t out_stride, hipStream_t st)
+template <typename VT>
+static void launch_ocv_wta_t(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+                             size_t out_stride, hipStream_t st)
 {
     const int D = g.D;
-    if (D <= 32) launch_ocv_wta_dpl<2>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 64) launch_ocv_wta_dpl<4>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 128) launch_ocv_wta_dpl<8>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 256) launch_ocv_wta_dpl<16>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_dpl<32>(vols, vol_elems, ndir, g, out, out_stride, st);
+    if (D <= 32) launch_ocv_wta_dpl<2, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 64) launch_ocv_wta_dpl<4, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 128) launch_ocv_wta_dpl<8, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else if (D <= 256) launch_ocv_wta_dpl<16, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_dpl<32, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+}
+
+// vols: int16 volumes, or int32 when g.wide (see ocv_volume_bytes)
+hipError_t launch_ocv_wta(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+                          size_t out_stride, hipStream_t st)
+{
+    if (g.wide) launch_ocv_wta_t<int32_t>(vols, vol_elems, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_t<int16_t>(vols, vol_elems, ndir, g, out, out_stride, st);
     return hipGetLastError();
 }
 

@@ -44,8 +44,8 @@ hipError_t launch_depth_points(const float*, size_t, int, int, const float*, dou
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
-hipError_t launch_ocv_paths(const int16_t*, int16_t*, size_t, const Geom&, int, hipStream_t);
-hipError_t launch_ocv_wta(const int16_t*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
+hipError_t launch_ocv_paths(const int16_t*, void*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
 }  // namespace sgm
 
 using sgm::Geom;
@@ -85,6 +85,13 @@ int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
         g.P1 = p.p1 > 0 ? p.p1 : 2;
         g.P2 = std::max(p.p2 > 0 ? p.p2 : 5, g.P1 + 1);
         g.subpix = 1; g.lr = 1;
+        // A pixel cost is <= 2*ftzero + 63 (BT of the prefiltered image + raw BT >> 2), so
+        // C = box sum + P2 stays in int16 below this bound, and then every path cost lies in
+        // [C - P2, C]: int16 volumes are exact. Above it C may wrap (OpenCV's CostType) and a
+        // path cost can leave int16, while OpenCV adds the int value into S: int32 volumes.
+        const long long cmax = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63) + g.P2;
+        const char* wide_env = std::getenv("SGM_OCV_WIDE");
+        g.wide = cmax > 32767 || (wide_env && std::atoi(wide_env) != 0);
     }
     g.uniq = p.uniqueness_ratio >= 0 ? p.uniqueness_ratio : 10;
     g.disp12 = p.disp12_max_diff > 0 ? p.disp12_max_diff : 1;
@@ -277,10 +284,11 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.planes = take(WH * 4);
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
-        l.ovol_elems = align_up(cells * 2) / 2;
-        // + slack: the path kernel's trash slots (64 lanes x 32 int16) and the WTA's last pixel
+        const size_t es = g.wide ? 4 : 2;          // int32 / int16 path volumes (Geom::wide)
+        l.ovol_elems = align_up(cells * es) / es;
+        // + slack: the path kernel's trash slots (64 lanes x 32 values) and the WTA's last pixel
         // group of the last row, which reads 3 pixels past the volume
-        l.ovols = take(l.ovol_elems * 2 * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 4096 + (size_t)8 * g.D);
+        l.ovols = take(es * (l.ovol_elems * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 64 * 32 + (size_t)8 * g.D));
     }
     l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
@@ -406,7 +414,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         const int ndir = fullDP ? 8 : 5;
         int16_t* A = (int16_t*)(ws + l.bufA);
         int16_t* B = (int16_t*)(ws + l.bufB);
-        int16_t* V = (int16_t*)(ws + l.ovols);
+        void* V = ws + l.ovols;
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
         HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, g, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
         rec.begin("ocv_paths", 2 * cells * (ndir + 1));

@@ -38,6 +38,7 @@ struct Geom {
     int subpix, lr;         // census: subpixel / LR-check flags (OCV: 1, 1)
     int invalid;            // (minD - 1) * 16
     int SW2, SH2, ftzero;   // OCV: SAD half window, prefilter cap
+    int wide;               // OCV: a cost may leave int16 -> int32 path volumes (exact S)
 };
 
 // Direction r = (rx, ry): L_r(p) depends on L_r(p - r). Engine volume order.

@@ -39,7 +39,7 @@ def _images(rng, synth, h, w, minD, D, kind, seed):
 def _case(pkg, seed):
     rng = np.random.default_rng(10_000 + seed)
     mode = [pkg.MODE_CENSUS8, pkg.MODE_OCV_SGBM5, pkg.MODE_OCV_HH8][seed % 3]
-    D = int(rng.choice([16, 32, 48, 64, 80, 96, 128, 144, 256]))
+    D = int(rng.choice([16, 32, 48, 64, 80, 96, 128, 144, 256, 272, 400, 512]))
     minD = int(rng.integers(-12, 13))
     span = max(D + minD, 0)
     h = int(rng.choice([1, 2, 3, 7, 16, 23, 40]))

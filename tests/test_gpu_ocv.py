@@ -100,6 +100,31 @@ def test_ocv_saturated_sums(engine, oracle, pkg, mode, uniq):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("force", ["", "1"], ids=["auto", "forced"])
+def test_ocv_wide_path_costs(engine, oracle, synth, pkg, monkeypatch, mode, force):
+    """Boxes whose sums can wrap int16 (21x21, preFilterCap 62): OpenCV's CostType cost
+    volume wraps, a path cost can leave int16, and S adds the int values — the engine keeps
+    int32 path volumes there (Geom::wide, automatic from the parameters). `forced` runs an
+    ordinary configuration through the int32 volumes too (SGM_OCV_WIDE=1)."""
+    if force:
+        monkeypatch.setenv("SGM_OCV_WIDE", force)
+        kw = dict(min_disparity=-4, num_disparities=48, block_size=5)
+        left, right, _ = synth.stereo_pair(37, 160, 0, 48, seed=5)
+    else:
+        kw = dict(min_disparity=-4, num_disparities=48, block_size=21, p1=106, p2=834, prefilter_cap=62,
+                  uniqueness_ratio=99, disp12_max_diff=5)
+        rng = np.random.default_rng(871)
+        left = np.full((9, 118), 90, dtype=np.uint8)
+        left[:, ::3] = rng.integers(0, 256, (9, 40), dtype=np.uint8)
+        right = np.roll(left, -3, axis=1)
+    p = pkg.default_params(mode, speckle_window_size=0, **kw)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
 def test_ocv_small_images_bottom_rows(engine, oracle, pkg):
     """Heights below the SAD window (every row hits OpenCV's no-recompute rule)."""
     rng = np.random.default_rng(7)
