@@ -106,3 +106,29 @@ def test_fuzz_tiled_exact(engine, oracle, synth, pkg, seed):
     got = engine.match_tiled_exact(left, right, bands)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
     assert np.array_equal(got, ref), f"{bands} bands, {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 2, 1)))
+def test_fuzz_post_filters(engine, oracle, seed):
+    """medianBlur(3) and filterSpeckles on random disparity images: piecewise-constant
+    blobs, ramps and noise of random sizes, newVal / maxSize / maxDiff drawn at random."""
+    rng = np.random.default_rng(50_000 + seed)
+    h, w = int(rng.integers(1, 150)), int(rng.integers(1, 300))
+    kind = int(rng.integers(0, 3))
+    if kind == 0:       # blobs: a coarse random grid upsampled, plus sparse noise
+        cy, cx = max(h // int(rng.integers(1, 12)), 1), max(w // int(rng.integers(1, 12)), 1)
+        coarse = rng.integers(-40, 400, (h // cy + 1, w // cx + 1))
+        disp = np.repeat(np.repeat(coarse, cy, 0), cx, 1)[:h, :w]
+        m = rng.random((h, w)) < 0.05
+        disp = np.where(m, rng.integers(-40, 400, (h, w)), disp)
+    elif kind == 1:     # ramps: neighbours differ by small steps
+        disp = (np.add.outer(np.arange(h) * int(rng.integers(0, 4)), np.arange(w) * int(rng.integers(0, 4))) % 500) - 20
+    else:
+        disp = rng.integers(-40, 400, (h, w))
+    disp = disp.astype(np.int16)
+    new_val = int(rng.choice([-16, -32, 0, int(disp.min())]))
+    max_size, max_diff = int(rng.choice([0, 1, 5, 30, 100, 1000])), int(rng.choice([0, 1, 16, 32, 64]))
+    assert np.array_equal(engine.median3(disp), oracle.median3(disp))
+    got = engine.filter_speckles(disp, new_val, max_size, max_diff)
+    ref = oracle.filter_speckles(disp, new_val, max_size, max_diff)
+    assert np.array_equal(got, ref), f"{h}x{w} kind {kind} new {new_val} size {max_size} diff {max_diff}"
