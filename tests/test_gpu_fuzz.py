@@ -132,3 +132,39 @@ def test_fuzz_post_filters(engine, oracle, seed):
     got = engine.filter_speckles(disp, new_val, max_size, max_diff)
     ref = oracle.filter_speckles(disp, new_val, max_size, max_diff)
     assert np.array_equal(got, ref), f"{h}x{w} kind {kind} new {new_val} size {max_size} diff {max_diff}"
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 4, 1)))
+def test_fuzz_rectify(engine, oracle, seed):
+    """initUndistortRectifyMap + INTER_CUBIC remap with random intrinsics, distortion models
+    (0/4/5/8/12 coefficients), rotations and sizes: float32 maps and u8 output bit-exact."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(70_000 + seed)
+    w, h = int(rng.integers(2, 400)), int(rng.integers(2, 300))
+    f = float(rng.uniform(0.3, 2.0)) * w
+    K = np.array([[f, 0, w / 2 + rng.normal(0, 5)], [0, f * rng.uniform(0.95, 1.05), h / 2 + rng.normal(0, 5)],
+                  [0, 0, 1]], np.float64)
+    nd = int(rng.choice([0, 4, 5, 8, 12]))
+    Dd = rng.normal(0, 0.05, nd) * np.array([1, 0.5, 0.02, 0.02, 0.2, 0.2, 0.1, 0.1, 0.01, 0.01, 0.01, 0.01])[:nd]
+    a = rng.normal(0, 0.05, 3)
+    th = np.linalg.norm(a)
+    k = a / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    R = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    P = np.array([[f * rng.uniform(0.8, 1.1), 0, w / 2 + rng.normal(0, 8), -0.1 * f],
+                  [0, f * rng.uniform(0.8, 1.1), h / 2 + rng.normal(0, 8), 0], [0, 0, 1, 0]], np.float64)
+    mx = torch.empty((h, w), dtype=torch.float32, device="cuda")
+    my = torch.empty((h, w), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    engine.rectify_map(K, Dd, R, P, w, h, mx.data_ptr(), my.data_ptr(), w)
+    engine.synchronize()
+    rx, ry = oracle.rectify_map(K, Dd, R, P, w, h)
+    assert np.array_equal(mx.cpu().numpy().view(np.uint32), rx.view(np.uint32)), "map x"
+    assert np.array_equal(my.cpu().numpy().view(np.uint32), ry.view(np.uint32)), "map y"
+    src = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    ds = torch.from_numpy(src).cuda()
+    out = torch.empty((h, w), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    engine.remap_cubic(ds.data_ptr(), w, w, h, mx.data_ptr(), my.data_ptr(), w, w, h, out.data_ptr(), w)
+    engine.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.remap_cubic(src, rx, ry)), "remap"
