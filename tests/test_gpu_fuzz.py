@@ -168,3 +168,39 @@ def test_fuzz_rectify(engine, oracle, seed):
     engine.remap_cubic(ds.data_ptr(), w, w, h, mx.data_ptr(), my.data_ptr(), w, w, h, out.data_ptr(), w)
     engine.synchronize()
     assert np.array_equal(out.cpu().numpy(), oracle.remap_cubic(src, rx, ry)), "remap"
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 4, 1)))
+def test_fuzz_depth(engine, oracle, pkg, seed):
+    """DisparityImage packing and disparity -> depth / point cloud with random calibrations,
+    depth windows, colour channels and disparity images (float32 bit-exact)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(90_000 + seed)
+    h, w = int(rng.integers(1, 120)), int(rng.integers(1, 300))
+    f = float(rng.uniform(200, 2000))
+    cx, cy = w / 2 + rng.normal(0, 10), h / 2 + rng.normal(0, 10)
+    K = np.array([[f, 0, cx], [0, f, cy], [0, 0, 1]])
+    Pl = np.array([[f, 0, cx, 0], [0, f, cy, 0], [0, 0, 1, 0]])
+    Pr = Pl.copy()
+    Pr[0, 3] = -f * float(rng.uniform(0.03, 0.5))
+    Pr[0, 2] = cx + rng.normal(0, 3)
+    Q = oracle.calc_q(K, Pr, Pl)
+    d = (rng.integers(-40, 4000, (h, w)) / 16.0).astype(np.float32)
+    d[rng.random((h, w)) < 0.15] = 0
+    d[rng.random((h, w)) < 0.1] = 10000
+    lo = float(rng.choice([0.0, 0.1, 0.5]))
+    window = (lo, lo + float(rng.choice([0.5, 3.0, 50.0, 1e4])))
+    channels = int(rng.choice([0, 1, 3]))
+    color = None if channels == 0 else rng.integers(0, 256, (h, w) if channels == 1 else (h, w, 3), dtype=np.uint8)
+    depth, pts, rgba = pkg.disp_info_to_depth(engine, d, color, Q, *window)
+    rd, rp, rr = oracle.depth_points(d, Q, *window, color)
+    assert np.array_equal(depth.view(np.uint32), rd.view(np.uint32)), "depth"
+    assert np.array_equal(pts.view(np.uint32), rp.view(np.uint32)), f"{len(pts)} vs {len(rp)} points"
+    assert np.array_equal(rgba, rr), "colour"
+    d16 = rng.integers(-300, 4000, (h, w)).astype(np.int16)
+    src = torch.as_tensor(d16).cuda()
+    out = torch.empty((h, w), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    engine.disparity_to_msg(src.data_ptr(), w, w, h, window[0], window[1], out.data_ptr(), w)
+    engine.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.disparity_to_msg(d16, *window).view(np.uint32))
