@@ -204,3 +204,57 @@ def test_fuzz_depth(engine, oracle, pkg, seed):
     engine.disparity_to_msg(src.data_ptr(), w, w, h, window[0], window[1], out.data_ptr(), w)
     engine.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.disparity_to_msg(d16, *window).view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 8, 1)))
+def test_fuzz_fused_rectify_batch(engine, oracle, synth, pkg, seed):
+    """Raw frames rectified inside the census tiles (sgm_match_device_batch_rect) with random
+    raw / rectified sizes, calibrations, census parameters and frame counts: rectified images
+    and disparities equal the oracle's remap and match of them."""
+    torch = pytest.importorskip("torch")
+    from test_rectify_oracle import calib
+    rng = np.random.default_rng(110_000 + seed)
+    D = int(rng.choice([16, 32, 64, 128]))
+    minD = int(rng.integers(0, 8))
+    rh, rw = int(rng.integers(8, 120)), int(rng.integers(D + minD + 8, D + minD + 200))
+    h, w = max(int(rh * rng.uniform(0.8, 1.1)), 1), max(int(rw * rng.uniform(0.9, 1.1)), D + minD + 1)
+    KL, DL, RL, PL = calib(seed=int(rng.integers(0, 1000)), w=rw, h=rh)
+    KR, DR, RR, PR = calib(seed=int(rng.integers(0, 1000)), w=rw, h=rh)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=minD, p1=int(rng.integers(2, 20)),
+                           p2=int(rng.integers(30, 190)), uniqueness_ratio=int(rng.choice([0, 5, 15])),
+                           subpixel=int(rng.integers(0, 2)), lr_check=int(rng.integers(0, 2)),
+                           median=int(rng.integers(0, 2)))
+    engine.set_params(p)
+    maps = []
+    for K_, D_, R_, P_ in ((KL, DL, RL, PL), (KR, DR, RR, PR)):
+        mx = torch.empty((h, w), dtype=torch.float32, device="cuda")
+        my = torch.empty((h, w), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        engine.rectify_map(K_, D_, R_, P_, w, h, mx.data_ptr(), my.data_ptr(), w)
+        engine.synchronize()
+        maps.append((mx, my))
+    n = int(rng.integers(1, 5))
+    frames = [synth.stereo_pair(rh, rw, minD, D, seed=seed * 7 + i, with_truth=False)[:2] for i in range(n)]
+    dl = [torch.as_tensor(f[0]).cuda() for f in frames]
+    dr = [torch.as_tensor(f[1]).cuda() for f in frames]
+    out = torch.full((n, h, w), 777, dtype=torch.int16, device="cuda")
+    recl = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+    recr = torch.zeros((n, h, w), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    engine.set_rectification((maps[0][0].data_ptr(), maps[0][1].data_ptr()),
+                             (maps[1][0].data_ptr(), maps[1][1].data_ptr()), w, rw, rh)
+    try:
+        engine.match_device_batch_rect([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], w, h, rw,
+                                       [recl[i].data_ptr() for i in range(n)], [recr[i].data_ptr() for i in range(n)],
+                                       w, [out[i].data_ptr() for i in range(n)], w)
+        engine.synchronize()
+    finally:
+        engine.set_rectification()
+    rxl, ryl = oracle.rectify_map(KL, DL, RL, PL, w, h)
+    rxr, ryr = oracle.rectify_map(KR, DR, RR, PR, w, h)
+    op = to_oracle_params(oracle, p)
+    got, gl, gr = out.cpu().numpy(), recl.cpu().numpy(), recr.cpu().numpy()
+    for i, (l_raw, r_raw) in enumerate(frames):
+        el, er = oracle.remap_cubic(l_raw, rxl, ryl), oracle.remap_cubic(r_raw, rxr, ryr)
+        assert np.array_equal(gl[i], el) and np.array_equal(gr[i], er), f"frame {i} rectified"
+        assert np.array_equal(got[i], oracle.match(op, el, er)), f"frame {i} of {n} disparity"
