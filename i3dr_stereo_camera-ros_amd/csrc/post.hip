@@ -12,12 +12,9 @@ namespace sgm {
 
 __device__ __forceinline__ void sort2(int& a, int& b) { int t = min(a, b); b = max(a, b); a = t; }
 
-__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src, size_t sstride,
-                                                 int16_t* __restrict__ dst, size_t dstride, int W, int H)
+// median of the 3x3 neighbourhood of (x, y), replicate border
+__device__ __forceinline__ int median9(const int16_t* __restrict__ src, size_t sstride, int x, int y, int W, int H)
 {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= W || y >= H) return;
     int p[9];
     int n = 0;
 #pragma unroll
@@ -34,7 +31,16 @@ __global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src
     sort2(p[3], p[6]); sort2(p[1], p[4]); sort2(p[2], p[5]);
     sort2(p[4], p[7]); sort2(p[4], p[2]); sort2(p[6], p[4]);
     sort2(p[4], p[2]);
-    dst[(size_t)y * dstride + x] = (int16_t)p[4];
+    return p[4];
+}
+
+__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src, size_t sstride,
+                                                 int16_t* __restrict__ dst, size_t dstride, int W, int H)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= W || y >= H) return;
+    dst[(size_t)y * dstride + x] = (int16_t)median9(src, sstride, x, y, W, H);
 }
 
 hipError_t launch_median3(const int16_t* src, size_t sstride, int16_t* dst, size_t dstride, int W, int H,
@@ -104,8 +110,11 @@ __device__ __forceinline__ void luf_union(int* l, int a, int b)
         a = old;
     }
 }
-__global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d, size_t stride, int W, int H,
-                                                  int newVal, int maxDiff, int* __restrict__ lab, int* __restrict__ cnt)
+// med (optional): the unfiltered disparity; the tile then applies medianBlur(3) itself, writes
+// the filtered values to d and labels them (one launch less than median + speckle)
+__global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ med, size_t mstride, int16_t* d,
+                                                  size_t stride, int W, int H, int newVal, int maxDiff,
+                                                  int* __restrict__ lab, int* __restrict__ cnt)
 {
     __shared__ int l[kSpkTW * kSpkTH];
     __shared__ int lcnt[kSpkTW * kSpkTH];
@@ -113,7 +122,15 @@ __global__ __launch_bounds__(256) void k_spk_tile(const int16_t* __restrict__ d,
     const int x0 = blockIdx.x * kSpkTW, y0 = blockIdx.y * kSpkTH;
     for (int i = threadIdx.x; i < kSpkTW * kSpkTH; i += 256) {
         const int x = x0 + (i & (kSpkTW - 1)), y = y0 + i / kSpkTW;
-        const int dv = (x < W && y < H) ? d[(size_t)y * stride + x] : newVal;
+        int dv = newVal;
+        if (x < W && y < H) {
+            if (med) {
+                dv = median9(med, mstride, x, y, W, H);
+                d[(size_t)y * stride + x] = (int16_t)dv;
+            } else {
+                dv = d[(size_t)y * stride + x];
+            }
+        }
         v[i] = (int16_t)dv;
         l[i] = dv != newVal ? i : -1;
         lcnt[i] = 0;
@@ -208,13 +225,14 @@ __global__ __launch_bounds__(256) void k_spk_apply(int16_t* __restrict__ d, size
     }
 }
 
-hipError_t launch_speckle(int16_t* d, size_t stride, int W, int H, int newVal, int maxSize, int maxDiff,
-                          int* lab, int* cnt, hipStream_t st)
+// med != nullptr: medianBlur(3) of med into d first, inside the tile kernel
+hipError_t launch_speckle(const int16_t* med, size_t mstride, int16_t* d, size_t stride, int W, int H, int newVal,
+                          int maxSize, int maxDiff, int* lab, int* cnt, hipStream_t st)
 {
     const int n = W * H;
     dim3 grid((n + 255) / 256), block(256);
     const dim3 tiles((W + kSpkTW - 1) / kSpkTW, (H + kSpkTH - 1) / kSpkTH);
-    hipLaunchKernelGGL(k_spk_tile, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab, cnt);
+    hipLaunchKernelGGL(k_spk_tile, tiles, block, 0, st, med, mstride, d, stride, W, H, newVal, maxDiff, lab, cnt);
     hipLaunchKernelGGL(k_spk_border, tiles, block, 0, st, d, stride, W, H, newVal, maxDiff, lab);
     hipLaunchKernelGGL(k_spk_count, grid, block, 0, st, W, H, maxSize, lab, cnt);
     hipLaunchKernelGGL(k_spk_apply, grid, block, 0, st, d, stride, W, H, newVal, maxSize, lab, cnt);

@@ -37,7 +37,7 @@ hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const Census
                                const uint32_t*, int, size_t,
                                hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
-hipError_t launch_speckle(int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
+hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
 hipError_t launch_disp_to_msg(const int16_t*, size_t, int, int, float, float, float*, size_t, hipStream_t);
 hipError_t launch_depth_points(const float*, size_t, int, int, const float*, double, double, const uint8_t*, size_t,
@@ -358,15 +358,17 @@ int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
     const double WH = (double)g.W * g.H;
-    if (use_median(p)) {
+    const int16_t* raw = (const int16_t*)(ws + l.tmp) + tmp_off;
+    const bool med = use_median(p), spk = p.speckle_window_size > 0;
+    if (med && !spk) {
         rec.begin("median3", 4 * WH);
-        HIP_TRY(sgm::launch_median3((int16_t*)(ws + l.tmp) + tmp_off, g.W, dOut, out_stride, g.W, g.H, h->stream),
-                "median3");
+        HIP_TRY(sgm::launch_median3(raw, g.W, dOut, out_stride, g.W, g.H, h->stream), "median3");
     }
-    if (p.speckle_window_size > 0) {
-        rec.begin("speckle", 14 * WH);
-        HIP_TRY(sgm::launch_speckle(dOut, out_stride, g.W, g.H, g.invalid, p.speckle_window_size,
-                                    16 * p.speckle_range, (int*)(ws + l.lab), (int*)(ws + l.cnt), h->stream),
+    if (spk) {   // with a median, the speckle tiles apply it first (one launch less)
+        rec.begin(med ? "median3+speckle" : "speckle", (med ? 4 : 0) * WH + 14 * WH);
+        HIP_TRY(sgm::launch_speckle(med ? raw : nullptr, g.W, dOut, out_stride, g.W, g.H, g.invalid,
+                                    p.speckle_window_size, 16 * p.speckle_range, (int*)(ws + l.lab),
+                                    (int*)(ws + l.cnt), h->stream),
                 "speckle");
     }
     return SGM_OK;
@@ -1377,7 +1379,7 @@ static int debug_post(sgm_handle* h, int16_t* disp, int W, int H, int which, int
         HIP_TRY(sgm::launch_median3(a, W, b, W, W, H, h->stream), "median3");
         HIP_TRY(hipMemcpyAsync(disp, b, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     } else {
-        HIP_TRY(sgm::launch_speckle(a, W, W, H, nv, ms, md, lab, cnt, h->stream), "speckle");
+        HIP_TRY(sgm::launch_speckle(nullptr, 0, a, W, W, H, nv, ms, md, lab, cnt, h->stream), "speckle");
         HIP_TRY(hipMemcpyAsync(disp, a, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     }
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
