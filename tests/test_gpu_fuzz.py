@@ -258,3 +258,24 @@ def test_fuzz_fused_rectify_batch(engine, oracle, synth, pkg, seed):
         el, er = oracle.remap_cubic(l_raw, rxl, ryl), oracle.remap_cubic(r_raw, rxr, ryr)
         assert np.array_equal(gl[i], el) and np.array_equal(gr[i], er), f"frame {i} rectified"
         assert np.array_equal(got[i], oracle.match(op, el, er)), f"frame {i} of {n} disparity"
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 4, 1)))
+def test_fuzz_host_batch_and_overlap_tiles(engine, oracle, synth, pkg, seed):
+    """Every mode through sgm_match_batch (host buffers, a thread + stream per device; the
+    device list repeats device 0 to exercise the per-device workers) and, with a halo that
+    covers the whole frame, through the overlap tile mode, which is then exact."""
+    rng, mode, h, w, kw, kind = _case(pkg, 7000 + seed)
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    n = int(rng.integers(1, 5))
+    frames = [_images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed + 31 * i)
+              for i in range(n)]
+    outs = engine.match_batch([f[0] for f in frames], [f[1] for f in frames], devices=[0] * int(rng.integers(1, 3)))
+    op = to_oracle_params(oracle, p)
+    refs = [oracle.match(op, l, r) for l, r in frames]
+    for i in range(n):
+        assert np.array_equal(outs[i], refs[i]), f"batch frame {i} of {n}, mode {mode} {h}x{w} {kw} {kind}"
+    bands = int(rng.integers(1, min(h, 4) + 1))
+    got = engine.match_tiled(frames[0][0], frames[0][1], bands, h)
+    assert np.array_equal(got, refs[0]), f"overlap tiles, {bands} bands, halo {h}, mode {mode} {h}x{w} {kw} {kind}"
