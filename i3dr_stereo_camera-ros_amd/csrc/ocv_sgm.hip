@@ -560,8 +560,8 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
 
 // WTA of the OCV modes, one workgroup (4 waves) per image row, 16 lanes per pixel (4 pixels
 // per wave-instruction): lane p of a row holds d = p*DPL .. p*DPL + DPL - 1 of its pixel,
-// loaded as one DPL x int16 vector per volume (coalesced). Same decisions as OpenCV's loop
-// (SURVEY Appendix A.6): S = saturate(sum of the NDIR L's); best = first minimal d through
+// loaded as one DPL-value vector per volume (coalesced). Same decisions as OpenCV's loop
+// (SURVEY Appendix A.6): S = the saturating sums in OpenCV's pass order; best = first minimal d through
 // one 16-lane min over (S + 32768) * 512 + d; uniqueness per element (S may be any int16
 // here); S[best +- 1] through a per-row LDS slice; then the shared disp2 / LR epilogue.
 template <int DPL, int NDIR, typename VT>
