@@ -321,3 +321,20 @@ def test_oracle_reproduces_golden(oracle, name):
     for k, v in zip(z["param_names"], z["param_values"]):
         setattr(p, str(k), int(v))
     assert np.array_equal(oracle.match(p, z["left"], z["right"]), z["disp"])
+
+
+@pytest.mark.parametrize("uniq", [0, 10])
+def test_kat_all_sums_saturated_is_invalid(oracle, uniq):
+    """OpenCV's `Sval < minS` from minS = MAX_COST never fires when every S equals MAX_COST:
+    bestDisp stays -1 and the pixel is INVALID (and disp2 is not touched: the oracle must not
+    read disp2cost one past the row there)."""
+    w, minD, D = 90, -4, 48
+    p = oracle.make_params(oracle.MODE_OCV_SGBM5, min_disparity=minD, num_disparities=D, uniqueness_ratio=uniq)
+    width1 = oracle.effective(p, w, 3)["width1"]
+    S = np.full((3, width1, D), 32767, np.uint16)
+    S[1, ::3, 5] = 1000                        # some pixels have a real minimum
+    disp = oracle.wta(p, S, w)
+    invalid = (minD - 1) * 16
+    x0 = max(minD + D, 0)
+    assert (disp[0] == invalid).all() and (disp[2] == invalid).all()
+    assert (disp[1, x0:x0 + width1][::3] != invalid).any()
