@@ -196,10 +196,10 @@ __device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, con
     __syncthreads();
     for (int x = g.minX1 + tid; x < g.maxX1; x += nthr) {
         const int b = bst[x];
-        const int m = mins[x];
+        const int m = (int16_t)mins[x];     // minS is a CostType: negative once OCV costs wrap
         if (b >= 0 && m < 32767) {
             const int x2 = x - b - g.minD;
-            atomicMin(&key[x2], ((uint32_t)m << 16) | (uint32_t)(0xFFFF - x));
+            atomicMin(&key[x2], ((uint32_t)(m + 32768) << 16) | (uint32_t)(0xFFFF - x));
         }
     }
     __syncthreads();

@@ -125,6 +125,20 @@ def test_ocv_wide_path_costs(engine, oracle, synth, pkg, monkeypatch, mode, forc
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("seed", [3791, 4079, 4568])
+def test_ocv_negative_min_cost_disp2(engine, oracle, synth, pkg, seed):
+    """Fuzz cases (tests/test_gpu_fuzz.py seeds) where wrapped costs make a pixel's minS
+    negative: disp2's "cost > minS" update must compare signed CostType values."""
+    from test_gpu_fuzz import _case, _images
+    rng, mode, h, w, kw, kind = _case(pkg, seed)
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    left, right = _images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
 def test_ocv_small_images_bottom_rows(engine, oracle, pkg):
     """Heights below the SAD window (every row hits OpenCV's no-recompute rule)."""
     rng = np.random.default_rng(7)
