@@ -255,12 +255,35 @@ class Engine:
     def synchronize(self):
         self._check(self.lib.sgm_synchronize(self.h))
 
-    def match_batch(self, lefts, rights, devices=None):
+    def match_batch(self, lefts, rights, devices=None, outs=None):
+        """Host frames, sharded frame i -> devices[i % n] and streamed through pinned rings
+        (sgm_match_batch). Row-strided views (one common row stride per side) are passed
+        without a copy; `outs` (int16 arrays or row-strided views, one stride) are filled in
+        place when given."""
         n = len(lefts)
-        lefts = [np.ascontiguousarray(a, np.uint8) for a in lefts]
-        rights = [np.ascontiguousarray(a, np.uint8) for a in rights]
         h, w = lefts[0].shape
-        outs = [np.empty((h, w), np.int16) for _ in range(n)]
+
+        def rows(arrs, dtype):
+            arrs = [a if (a.dtype == dtype and a.ndim == 2 and a.strides[1] == a.itemsize and
+                          a.strides[0] % a.itemsize == 0) else np.ascontiguousarray(a, dtype) for a in arrs]
+            st = {a.strides[0] // a.itemsize for a in arrs}
+            if len(st) != 1:   # one stride per side: compact the odd ones out
+                arrs = [np.ascontiguousarray(a) for a in arrs]
+                st = {w}
+            return arrs, st.pop()
+
+        lefts, sl = rows(lefts, np.uint8)
+        rights, sr = rows(rights, np.uint8)
+        if sl != sr:
+            lefts = [np.ascontiguousarray(a) for a in lefts]
+            rights = [np.ascontiguousarray(a) for a in rights]
+            sl = w
+        if outs is None:
+            outs = [np.empty((h, w), np.int16) for _ in range(n)]
+        so = {a.strides[0] // 2 for a in outs}
+        if (len(so) != 1 or any(a.dtype != np.int16 or a.shape != (h, w) or a.strides[1] != 2 for a in outs)):
+            raise ValueError("outs must be int16 (h, w) row-strided arrays with one common row stride")
+        so = so.pop()
         arr = ctypes.c_void_p * max(n, 1)
         L = arr(*[a.ctypes.data for a in lefts])
         R = arr(*[a.ctypes.data for a in rights])
@@ -270,7 +293,7 @@ class Engine:
             nd = len(devices)
         else:
             devs, nd = None, 0
-        self._check(self.lib.sgm_match_batch(self.h, L, R, n, w, h, w, O, w, devs, nd))
+        self._check(self.lib.sgm_match_batch(self.h, L, R, n, w, h, sl, O, so, devs, nd))
         return outs
 
     def match_tiled(self, left, right, n_bands, halo, devices=None):

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -146,6 +148,17 @@ struct sgm_handle {
     std::vector<sgm_handle*> bands;
     hipStream_t stream2 = nullptr;
     hipEvent_t bev[4] = {};
+    // cross-call ordering: every call that uses the workspace records `done` on the stream it
+    // ran on, and the next call (whatever its stream) waits on it first
+    hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    // host-buffer frame streaming (sgm_match_batch): device + pinned rings, copy streams
+    void* io_dev = nullptr;
+    size_t io_dev_size = 0;
+    uint8_t* io_pin = nullptr;
+    size_t io_pin_size = 0;
+    hipStream_t up = nullptr, down = nullptr;
+    std::vector<hipEvent_t> io_ev;
 };
 
 namespace {
@@ -171,7 +184,24 @@ int ensure_stream(sgm_handle* h)
 {
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
     if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!h->done) HIP_TRY(hipEventCreateWithFlags(&h->done, hipEventDisableTiming), "hipEventCreate");
     if (!h->n_cu) HIP_TRY(hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->device), "attr");
+    return SGM_OK;
+}
+
+// Orders a call on stream `st` after the previous call that used the handle's workspace
+// (on any stream): the workspace (codes, volumes, scratch) is shared by all calls.
+int order_after_last(sgm_handle* h, hipStream_t st)
+{
+    if (h->done_stream && h->done_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->done, 0), "hipStreamWaitEvent");
+    return SGM_OK;
+}
+
+// Marks the end of a call's work on `st` (see order_after_last).
+int mark_done(sgm_handle* h, hipStream_t st)
+{
+    HIP_TRY(hipEventRecord(h->done, st), "hipEventRecord");
+    h->done_stream = st;
     return SGM_OK;
 }
 
@@ -204,6 +234,7 @@ int ensure_ws(sgm_handle* h, size_t bytes)
     h->items_key[1].clear();
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
+        if (h->done_stream) (void)hipEventSynchronize(h->done);
         (void)hipFree(h->ws.base);
         h->ws.base = nullptr;
         h->ws.size = 0;
@@ -430,6 +461,19 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
     return SGM_OK;
 }
 
+// Callbacks of a frame batch whose inputs arrive and outputs leave while it runs (the
+// host-buffer streaming of sgm_match_batch). Frames [f0, f0 + n):
+//   inputs       before the first launch that reads their input images;
+//   outputs_free before the first launch that writes their disparities;
+//   outputs_done after the last launch that writes them.
+// Each returns a status (non-zero aborts the batch).
+struct FrameHooks {
+    virtual int inputs(int f0, int n) = 0;
+    virtual int outputs_free(int f0, int n) = 0;
+    virtual int outputs_done(int f0, int n) = 0;
+    virtual ~FrameHooks() = default;
+};
+
 // Frames per pipelined launch: 2 (more path blocks than resident workgroup slots, so the
 // dispatcher balances the CUs) unless the batch is shorter; SGM_GROUP overrides (1..4).
 int batch_group(int n)
@@ -451,7 +495,8 @@ int batch_group(int n)
 // rectified images.
 int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* const* dLs,
                      const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride,
-                     uint8_t* const* rectLs = nullptr, uint8_t* const* rectRs = nullptr, size_t rect_stride = 0)
+                     uint8_t* const* rectLs = nullptr, uint8_t* const* rectRs = nullptr, size_t rect_stride = 0,
+                     FrameHooks* hooks = nullptr)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
@@ -505,6 +550,12 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         }
         return cf;
     };
+    // hooks of group k (no-ops without hooks)
+    auto hk_in = [&](int k) { return hooks ? hooks->inputs(k * G, frames_of(k)) : 0; };
+    auto hk_free = [&](int k) { return hooks ? hooks->outputs_free(k * G, frames_of(k)) : 0; };
+    auto hk_done = [&](int k) { return hooks ? hooks->outputs_done(k * G, frames_of(k)) : 0; };
+    int hrc = hk_in(0);
+    if (hrc) return hrc;
     if (h->rect_on) {           // remap + census of the first group, one launch
         rec.begin("rectify+census", (2 * WH + 16 * WH + 16 * WH) * frames_of(0));
         HIP_TRY(sgm::launch_census_tiles(census_frames(0), g.W, g.H, st), "rectify+census");
@@ -516,6 +567,10 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         }
     }
     for (int k = 0; k <= ng; k++) {
+        // this launch reads the inputs of group k + 1 (census in the tail) and writes the
+        // disparities of group k - 1 (WTA)
+        if (k + 1 < ng && ng > 1 && (hrc = hk_in(k + 1))) return hrc;
+        if (k > 0 && (hrc = hk_free(k - 1))) return hrc;
         if (k == ng) {
             rec.begin("wta_lr", (8 * cells + 2 * WH) * frames_of(k - 1));
             HIP_TRY(sgm::launch_census_wta(wta_frames(k - 1), l.vol_bytes, g, dst_stride, st), "wta");
@@ -537,6 +592,7 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
                 int rc = run_post(h, l, g, outs[k1 * G + f], out_stride, rec, (size_t)f * g.W * g.H);
                 if (rc) return rc;
             }
+            if ((hrc = hk_done(k1))) return hrc;
         }
     }
     rec.end();
@@ -548,6 +604,7 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
     if ((rc = ensure_stream(h))) return rc;
+    if ((rc = order_after_last(h, h->stream))) return rc;   // synchronous calls run on the handle's stream
     l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
     if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
@@ -604,6 +661,7 @@ void sgm_destroy(sgm_handle* h)
     if (hipSetDevice(h->device) == hipSuccess) {
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+        if (h->done_stream) (void)hipEventSynchronize(h->done);   // the last call on a caller's stream
         for (hipEvent_t e : h->bev) if (e) (void)hipEventDestroy(e);
         if (h->stream2) (void)hipStreamDestroy(h->stream2);
         if (h->ws.base) (void)hipFree(h->ws.base);
@@ -612,6 +670,12 @@ void sgm_destroy(sgm_handle* h)
         if (h->aux) (void)hipFree(h->aux);
         if (h->cubic_tab) (void)hipFree(h->cubic_tab);
         for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+        if (h->up) { (void)hipStreamSynchronize(h->up); (void)hipStreamDestroy(h->up); }
+        if (h->down) { (void)hipStreamSynchronize(h->down); (void)hipStreamDestroy(h->down); }
+        for (hipEvent_t e : h->io_ev) (void)hipEventDestroy(e);
+        if (h->io_dev) (void)hipFree(h->io_dev);
+        if (h->io_pin) (void)hipHostFree(h->io_pin);
+        if (h->done) (void)hipEventDestroy(h->done);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -660,7 +724,9 @@ int sgm_match_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W,
     if (rc) return rc;
     hipStream_t own = h->stream;
     if (stream) h->stream = (hipStream_t)stream;
-    rc = run_pipeline(h, l, g, dL, dR, stride, dOut, out_stride);
+    rc = order_after_last(h, h->stream);
+    if (!rc) rc = run_pipeline(h, l, g, dL, dR, stride, dOut, out_stride);
+    if (!rc) rc = mark_done(h, h->stream);
     h->stream = own;
     return rc;
 }
@@ -692,11 +758,14 @@ int sgm_match_device_batch_rect(sgm_handle* h, const uint8_t* const* dLs, const 
     if (rc) return rc;
     hipStream_t own = h->stream;
     if (stream) h->stream = (hipStream_t)stream;
-    if (pipelined) {
+    rc = order_after_last(h, h->stream);
+    if (rc) {
+    } else if (pipelined) {
         rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride, rectLs, rectRs, rect_stride);
     } else {
         for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
     }
+    if (!rc) rc = mark_done(h, h->stream);
     h->stream = own;
     return rc;
 }
@@ -905,22 +974,316 @@ static int run_on_subs(sgm_handle* h, const std::vector<int>& devs, F job)
     return SGM_OK;
 }
 
+// ------------------------------------------------------- host-buffer frame streaming ----
+// sgm_match_batch on one device (SURVEY §8(e) "frame batch": one host thread + stream set
+// per device, pinned host rings). The device's frames flow through rings of pinned host
+// slots and device slots (io_ring_frames) while the pipelined batch runs:
+//   packer thread    user L/R rows -> pinned input slot (once that slot's previous H2D is done)
+//   driver (caller)  H2D on `up` -> census / paths / WTA / post on the compute stream -> D2H on `down`
+//   unpacker thread  pinned output slot -> user disparity rows (once its D2H is done)
+// so the host copies, both PCIe directions and the kernels overlap; the driver only blocks
+// when a ring is full. The copies run as blit kernels on high-priority streams, so they
+// slip in between the pipeline launch's workgroups instead of waiting for it to end
+// (C3 host-buffer batch: 530 -> 629 pairs/s against 664 device-resident). Reference pattern: the per-frame upload/match/download of
+// matcherOpenCVBlockCuda.cpp:27-30, driven per frame by generate_disparity.cpp:334-368.
+namespace {
+
+constexpr int kIoRing = 16;   // max frames per ring
+
+// Frames per ring: up to 256 MB of pinned staging per device, at least 8 frames (> 2 groups
+// of sgm::kMaxGroup frames, so a launch never waits on its own group's slots).
+int io_ring_frames(size_t WH) { return (int)std::max<size_t>(8, std::min<size_t>(kIoRing, (256u << 20) / (4 * WH))); }
+
+struct HostStreamer final : FrameHooks {
+    sgm_handle* h = nullptr;
+    int W = 0, H = 0;
+    size_t stride = 0, out_stride = 0, WH = 0;
+    std::vector<const uint8_t*> L, R;   // this device's frames, local order
+    std::vector<int16_t*> O;
+    int n = 0;
+    int ring = kIoRing;              // frames per ring (io_ring_frames)
+    uint8_t* din = nullptr;             // device ring: ring x (left | right)
+    int16_t* dout = nullptr;            // device ring: ring x disparity
+    uint8_t* pin = nullptr;             // pinned ring: ring x (left | right)
+    int16_t* pout = nullptr;            // pinned ring: ring x disparity
+    hipEvent_t *ev_h2d = nullptr, *ev_free = nullptr, *ev_d2h = nullptr, ev_ready = nullptr;   // per slot
+    std::mutex m;
+    std::condition_variable cv;
+    // progress counters (frames): packed into pinned slots, H2D issued, read by an issued
+    // launch, D2H issued, copied to the caller
+    int packed = 0, uploaded = 0, consumed = 0, d2h_issued = 0, unpacked = 0;
+    int err = SGM_OK;
+    std::string err_msg;
+    bool stop = false;
+    // SGM_IO_TRACE=1: seconds spent copying / waiting per role, printed after the batch
+    double t_pack = 0, t_pack_wait = 0, t_unpack = 0, t_unpack_wait = 0, t_drv_in = 0, t_drv_out = 0;
+    double t_api_in = 0, t_api_free = 0, t_api_out = 0;   // inside the HIP calls of each hook
+    static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+    void set_error(int code, const std::string& msg)
+    {
+        std::lock_guard<std::mutex> lk(m);
+        if (!err) { err = code; err_msg = msg; }
+        stop = true;
+        cv.notify_all();
+    }
+    int hip_error(hipError_t e, const char* where)
+    {
+        set_error(SGM_ERR_DEVICE, std::string(where) + ": " + hipGetErrorString(e));
+        return SGM_ERR_DEVICE;
+    }
+    // blocks until pred() or a stop; false on stop
+    template <typename P> bool wait_for(P pred)
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stop || pred(); });
+        return !stop;
+    }
+    void advance(int& counter, int v)
+    {
+        { std::lock_guard<std::mutex> lk(m); counter = v; }
+        cv.notify_all();
+    }
+
+    void packer()
+    {
+        if (hipSetDevice(h->device) != hipSuccess) { set_error(SGM_ERR_DEVICE, "hipSetDevice"); return; }
+        for (int j = 0; j < n; j++) {
+            const int slot = j % ring;
+            double t0 = now();
+            if (j >= ring) {            // the slot's previous frame must have left for the device
+                if (!wait_for([&] { return uploaded > j - ring; })) return;
+                hipError_t e = hipEventSynchronize(ev_h2d[slot]);
+                if (e != hipSuccess) { hip_error(e, "packer: hipEventSynchronize"); return; }
+            }
+            double t1 = now();
+            t_pack_wait += t1 - t0;
+            uint8_t* dst = pin + (size_t)slot * 2 * WH;
+            if (stride == (size_t)W) {
+                std::memcpy(dst, L[j], WH);
+                std::memcpy(dst + WH, R[j], WH);
+            } else {
+                for (int y = 0; y < H; y++) std::memcpy(dst + (size_t)y * W, L[j] + (size_t)y * stride, W);
+                for (int y = 0; y < H; y++) std::memcpy(dst + WH + (size_t)y * W, R[j] + (size_t)y * stride, W);
+            }
+            t_pack += now() - t1;
+            advance(packed, j + 1);
+        }
+    }
+
+    void unpacker()
+    {
+        if (hipSetDevice(h->device) != hipSuccess) { set_error(SGM_ERR_DEVICE, "hipSetDevice"); return; }
+        for (int j = 0; j < n; j++) {
+            double t0 = now();
+            if (!wait_for([&] { return d2h_issued > j; })) return;
+            const int slot = j % ring;
+            hipError_t e = hipEventSynchronize(ev_d2h[slot]);
+            if (e != hipSuccess) { hip_error(e, "unpacker: hipEventSynchronize"); return; }
+            double t1 = now();
+            t_unpack_wait += t1 - t0;
+            const int16_t* src = pout + (size_t)slot * WH;
+            if (out_stride == (size_t)W) {
+                std::memcpy(O[j], src, WH * 2);
+            } else {
+                for (int y = 0; y < H; y++) std::memcpy(O[j] + (size_t)y * out_stride, src + (size_t)y * W, 2 * (size_t)W);
+            }
+            t_unpack += now() - t1;
+            advance(unpacked, j + 1);
+        }
+    }
+
+    int inputs(int f0, int nf) override
+    {
+        // every launch issued so far has read the inputs of the frames before f0
+        for (int j = consumed; j < f0; j++) {
+            hipError_t e = hipEventRecord(ev_free[j % ring], h->stream);
+            if (e != hipSuccess) return hip_error(e, "hipEventRecord");
+        }
+        consumed = std::max(consumed, f0);
+        for (int j = f0; j < f0 + nf; j++) {
+            const double t0 = now();
+            if (!wait_for([&] { return packed > j; })) return err ? err : SGM_ERR_DEVICE;
+            const double t1 = now();
+            t_drv_in += t1 - t0;
+            const int slot = j % ring;
+            hipError_t e = hipSuccess;
+            if (j >= ring) e = hipStreamWaitEvent(h->up, ev_free[slot], 0);   // device slot read by its census
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(din + (size_t)slot * 2 * WH, pin + (size_t)slot * 2 * WH, 2 * WH,
+                                   hipMemcpyHostToDevice, h->up);
+            if (e == hipSuccess) e = hipEventRecord(ev_h2d[slot], h->up);
+            if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, ev_h2d[slot], 0);
+            if (e != hipSuccess) return hip_error(e, "frame upload");
+            t_api_in += now() - t1;
+            advance(uploaded, j + 1);
+        }
+        return SGM_OK;
+    }
+
+    int outputs_free(int f0, int nf) override
+    {
+        const double t0 = now();
+        struct Acc { double& a; double t; ~Acc() { a += now() - t; } } acc{t_api_free, t0};
+        // The device slot is free once its previous frame reached the caller (the unpacker
+        // saw that frame's D2H complete). A host-side wait: a stream wait on the copy
+        // stream's event would block the host inside HIP until that copy is submitted.
+        for (int j = std::max(f0, ring); j < f0 + nf; j++) {
+            if (d2h_issued <= j - ring) { set_error(SGM_ERR_ARG, "output ring overrun"); return SGM_ERR_ARG; }
+            if (!wait_for([&] { return unpacked > j - ring; })) return err ? err : SGM_ERR_DEVICE;
+        }
+        return SGM_OK;
+    }
+
+    int outputs_done(int f0, int nf) override
+    {
+        hipError_t e = hipEventRecord(ev_ready, h->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->down, ev_ready, 0);
+        if (e != hipSuccess) return hip_error(e, "output event");
+        for (int j = f0; j < f0 + nf; j++) {
+            const int slot = j % ring;
+            // the pinned slot's previous frame must have reached the caller's buffer
+            const double t0 = now();
+            if (j >= ring && !wait_for([&] { return unpacked > j - ring; })) return err ? err : SGM_ERR_DEVICE;
+            t_drv_out += now() - t0;
+            const double t1 = now();
+            e = hipMemcpyAsync(pout + (size_t)slot * WH, dout + (size_t)slot * WH, WH * 2, hipMemcpyDeviceToHost,
+                               h->down);
+            if (e == hipSuccess) e = hipEventRecord(ev_d2h[slot], h->down);
+            if (e != hipSuccess) return hip_error(e, "frame download");
+            t_api_out += now() - t1;
+            advance(d2h_issued, j + 1);
+        }
+        return SGM_OK;
+    }
+};
+
+// Device + pinned rings and the copy streams / events of a handle (kept across calls).
+int ensure_io(sgm_handle* h, size_t WH)
+{
+    const int ring = io_ring_frames(WH);
+    const size_t dev_bytes = align_up((size_t)ring * 2 * WH) + align_up((size_t)ring * 2 * WH);
+    const size_t pin_bytes = (size_t)ring * 4 * WH;
+    // copy streams at the highest priority: when a copy runs as a blit kernel, its few
+    // workgroups are dispatched ahead of the pipeline launch's queued ones
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    const char* pe = std::getenv("SGM_IO_PRIO");
+    const int prio = (pe && std::atoi(pe) == 0) ? 0 : hi;
+    if (!h->up) HIP_TRY(hipStreamCreateWithPriority(&h->up, hipStreamNonBlocking, prio), "hipStreamCreate");
+    if (!h->down) HIP_TRY(hipStreamCreateWithPriority(&h->down, hipStreamNonBlocking, prio), "hipStreamCreate");
+    while (h->io_ev.size() < 3 * kIoRing + 1) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        h->io_ev.push_back(e);
+    }
+    if (h->io_dev_size < dev_bytes) {
+        if (h->io_dev) { (void)hipFree(h->io_dev); h->io_dev = nullptr; h->io_dev_size = 0; }
+        HIP_TRY(hipMalloc(&h->io_dev, dev_bytes), "hipMalloc frame ring");
+        h->io_dev_size = dev_bytes;
+    }
+    if (h->io_pin_size < pin_bytes) {
+        if (h->io_pin) { (void)hipHostFree(h->io_pin); h->io_pin = nullptr; h->io_pin_size = 0; }
+        HIP_TRY(hipHostMalloc((void**)&h->io_pin, pin_bytes, hipHostMallocDefault), "hipHostMalloc frame ring");
+        h->io_pin_size = pin_bytes;
+    }
+    return SGM_OK;
+}
+
+// The frames `idx` of a host batch on one device handle (census mode: the pipelined
+// batch of run_batch_census; other modes: one pipeline per frame), streamed as above.
+int stream_host_frames(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights,
+                       int16_t* const* disps, const std::vector<int>& idx, int W, int H, size_t stride,
+                       size_t out_stride)
+{
+    const int n = (int)idx.size();
+    if (n == 0) return SGM_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    Geom g;
+    int rc = make_geom(h->params, W, H, g, h->err);
+    if (rc) return rc;
+    const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2 && g.width1 > 0;
+    Layout l;
+    if ((rc = prepare(h, W, H, false, g, l, pipelined ? batch_group(n) : 0))) return rc;
+    const size_t WH = (size_t)W * H;
+    if ((rc = ensure_io(h, WH))) return rc;
+    HostStreamer s;
+    s.h = h; s.W = W; s.H = H; s.stride = stride; s.out_stride = out_stride; s.WH = WH; s.n = n;
+    for (int i : idx) { s.L.push_back(lefts[i]); s.R.push_back(rights[i]); s.O.push_back(disps[i]); }
+    const int ring = s.ring = io_ring_frames(WH);
+    s.din = (uint8_t*)h->io_dev;
+    s.dout = (int16_t*)((char*)h->io_dev + align_up((size_t)ring * 2 * WH));
+    s.pin = h->io_pin;
+    s.pout = (int16_t*)(h->io_pin + (size_t)ring * 2 * WH);
+    s.ev_h2d = h->io_ev.data();
+    s.ev_free = h->io_ev.data() + kIoRing;
+    s.ev_d2h = h->io_ev.data() + 2 * kIoRing;
+    s.ev_ready = h->io_ev[3 * kIoRing];
+    std::vector<const uint8_t*> dL(n), dR(n);
+    std::vector<int16_t*> dO(n);
+    for (int j = 0; j < n; j++) {
+        dL[j] = s.din + (size_t)(j % ring) * 2 * WH;
+        dR[j] = dL[j] + WH;
+        dO[j] = s.dout + (size_t)(j % ring) * WH;
+    }
+    const double t_start = HostStreamer::now();
+    std::thread tp([&] { s.packer(); });
+    std::thread tu([&] { s.unpacker(); });
+    if (pipelined) {
+        rc = run_batch_census(h, l, g, dL.data(), dR.data(), n, (size_t)W, dO.data(), (size_t)W, nullptr, nullptr, 0,
+                              &s);
+    } else {
+        for (int j = 0; j < n && !rc; j++) {
+            if (!(rc = s.inputs(j, 1)) && !(rc = s.outputs_free(j, 1)) &&
+                !(rc = run_pipeline(h, l, g, dL[j], dR[j], (size_t)W, dO[j], (size_t)W)))
+                rc = s.outputs_done(j, 1);
+        }
+    }
+    if (rc) {
+        std::string msg = h->err;
+        s.set_error(rc, msg);
+    }
+    const double t_end = HostStreamer::now();
+    tp.join();
+    tu.join();
+    if (const char* tr = std::getenv("SGM_IO_TRACE"); tr && std::atoi(tr)) {
+        (void)hipStreamSynchronize(h->stream);
+        std::fprintf(stderr,
+                     "[sgm io] dev %d frames %d: driver issue %.2f ms (waits: packed %.2f, unpacked %.2f) | packer copy %.2f "
+                     "wait %.2f | unpacker copy %.2f wait %.2f | api h2d %.2f free %.2f d2h %.2f | total %.2f ms\n",
+                     h->device, n, (t_end - t_start) * 1e3, s.t_drv_in * 1e3, s.t_drv_out * 1e3, s.t_pack * 1e3,
+                     s.t_pack_wait * 1e3, s.t_unpack * 1e3, s.t_unpack_wait * 1e3, s.t_api_in * 1e3, s.t_api_free * 1e3,
+                     s.t_api_out * 1e3, (HostStreamer::now() - t_start) * 1e3);
+    }
+    const hipError_t e1 = hipStreamSynchronize(h->stream), e2 = hipStreamSynchronize(h->up),
+                     e3 = hipStreamSynchronize(h->down);
+    if (s.err) return fail(h, s.err, s.err_msg.empty() ? h->err : s.err_msg);
+    if (e1 != hipSuccess) return hip_fail(h, e1, "hipStreamSynchronize");
+    if (e2 != hipSuccess) return hip_fail(h, e2, "hipStreamSynchronize up");
+    if (e3 != hipSuccess) return hip_fail(h, e3, "hipStreamSynchronize down");
+    return mark_done(h, h->stream);
+}
+
+}  // namespace
+
 extern "C" {
 
 int sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights, int n_frames, int W,
                     int H, size_t stride, int16_t* const* disps, size_t out_stride, const int* devices, int n_dev)
 {
     if (!h || !lefts || !rights || !disps || n_frames < 0) return SGM_ERR_ARG;
+    if (W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W) return fail(h, SGM_ERR_ARG, "bad sizes");
+    for (int i = 0; i < n_frames; i++)
+        if (!lefts[i] || !rights[i] || !disps[i]) return fail(h, SGM_ERR_ARG, "null frame pointer");
+    if (n_frames == 0) return SGM_OK;
     std::vector<int> devs;
     int rc = open_subs(h, devices, n_dev, devs);
     if (rc) return rc;
     const int nd = (int)devs.size();
     return run_on_subs(h, devs, [&](int t, sgm_handle* sub) {
-        for (int i = t; i < n_frames; i += nd) {
-            int r = sgm_match(sub, lefts[i], rights[i], W, H, stride, disps[i], out_stride);
-            if (r) return r;
-        }
-        return (int)SGM_OK;
+        std::vector<int> mine;
+        for (int i = t; i < n_frames; i += nd) mine.push_back(i);
+        return stream_host_frames(sub, lefts, rights, disps, mine, W, H, stride, out_stride);
     });
 }
 
@@ -1295,7 +1658,7 @@ int sgm_debug_census(sgm_handle* h, const uint8_t* img, int W, int H, size_t str
     if (!h || !img || !out || W <= 0 || H <= 0 || stride < (size_t)W) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = ensure_stream(h);
-    if (rc) return rc;
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
     const size_t WH = (size_t)W * H;
     if ((rc = ensure_ws(h, align_up(WH) + WH * 8))) return rc;
     char* ws = (char*)h->ws.base;
@@ -1366,7 +1729,7 @@ static int debug_post(sgm_handle* h, int16_t* disp, int W, int H, int which, int
     if (!h || !disp || W <= 0 || H <= 0) return SGM_ERR_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = ensure_stream(h);
-    if (rc) return rc;
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
     const size_t WH = (size_t)W * H;
     if ((rc = ensure_ws(h, align_up(WH * 2) * 2 + align_up(WH * 4) * 2))) return rc;
     char* ws = (char*)h->ws.base;

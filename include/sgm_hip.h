@@ -101,14 +101,22 @@ int  sgm_match(sgm_handle* h, const uint8_t* left, const uint8_t* right,
                int16_t* disp, size_t out_stride);
 
 /* Device buffers in/out (already resident in HBM), asynchronous on `stream` (hipStream_t,
- * NULL = the handle's own stream). The handle's device must own the buffers.              */
+ * NULL = the handle's own stream). The handle's device must own the buffers. Calls on one
+ * handle share its workspace, so each call is ordered after the previous one whatever the
+ * streams (an event recorded at the end of every call is waited on at the start of the next);
+ * use one handle per concurrent stream to overlap matches.                                  */
 int  sgm_match_device(sgm_handle* h, const uint8_t* d_left, const uint8_t* d_right,
                       int width, int height, size_t stride,
                       int16_t* d_disp, size_t out_stride, void* stream);
 
-/* Frame batch, sharded frame i -> devices[i % n_dev] with one host thread + stream per
- * device (SURVEY §8e "frame batch"). Host buffers; synchronous; no cross-device traffic.
- * n_dev <= 0 or devices == NULL: all visible devices.                                      */
+/* Frame batch, sharded frame i -> devices[i % n_dev] (SURVEY §8e "frame batch"). Each
+ * device gets a driver thread, a packer and an unpacker thread, a compute stream and two
+ * high-priority copy streams: its frames stream through pinned host rings (user rows ->
+ * pinned -> H2D -> pipelined census batch / per-frame OCV pipeline -> D2H -> user rows), so
+ * host copies, PCIe and kernels overlap. Host buffers with one row stride per side (stride,
+ * out_stride in elements); synchronous; no cross-device traffic. n_dev <= 0 or
+ * devices == NULL: all visible devices; a device may be listed more than once (one handle
+ * per entry). Results equal sgm_match per frame.                                            */
 int  sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* const* rights,
                      int n_frames, int width, int height, size_t stride,
                      int16_t* const* disps, size_t out_stride,
