@@ -42,6 +42,40 @@ static inline int imax(int a, int b) { return a > b ? a : b; }
 static inline int iclamp(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 static inline int16_t sat16(int v) { return (int16_t)iclamp(v, SHRT_MIN, SHRT_MAX); }
 
+/* ======================================================================================
+ * OpenCV build variants (oracle switches; DESIGN.md §3 "OpenCV semantics targets").
+ * The reference pins OpenCV only by ROS distro (melodic -> 3.2.0, noetic -> 4.2.0;
+ * .github/workflows/ros-build.yml:14-21, CMakeLists.txt:48-51), and computeDisparitySGBM
+ * differs between versions and between its scalar and CV_SIMD branches. Default (0) is the
+ * restatement the GPU engine reproduces: the scalar branch with the column-0 update of the
+ * refactored 4.x loop. Bits:
+ *   SGMREF_OCV_COL0_LEGACY  the 3.x loop `for (x = D; x < width1*D; x += D)`: for y > 0 the
+ *                           vertical running sum never updates C' column 0 (x = minX1), so it
+ *                           keeps its row-0 value (MODE_SGBM, one C row buffer) or the P2
+ *                           initialisation (MODE_HH, one C row per image row).
+ *   SGMREF_OCV_SIMD_SAT     the CV_SIMD (SSE2 / universal-intrinsic) branches, taken by every
+ *                           x86-64 build: int16 saturating adds/subs in the y > 0 horizontal and
+ *                           vertical running sums ((h - sub) + add, (C - hsub) + h), in the path
+ *                           recurrence (L = sat(sat(min - delta) + C), Lp(d+-1) + P1 saturated,
+ *                           delta = (short)(minLr + P2)), Lr and minLr kept as the saturated
+ *                           int16 values, and S = sat(sat(S + sat(L0+L1)) + sat(L2+L3)) (+ the
+ *                           fifth path saturated alone). Scalar: int arithmetic, int16 wrapping
+ *                           stores, S += saturate_cast(L0+L1+L2+L3). They agree while no box
+ *                           sum or path cost leaves int16.
+ *   SGMREF_OCV_LANE_TIE     MODE_SGBM's SSE2 WTA (3.x: per-lane strict minima over 8 int16
+ *                           lanes, then LSBTab of the lanes holding the minimum): among equal
+ *                           minimal S the winner is the one in the lowest lane (d mod 8), then
+ *                           the smallest d in that lane, instead of the smallest d.
+ * ====================================================================================== */
+#define SGMREF_OCV_COL0_LEGACY 1
+#define SGMREF_OCV_SIMD_SAT 2
+#define SGMREF_OCV_LANE_TIE 4
+static int g_ocv_compat = 0;
+void sgmref_set_ocv_compat(int flags) { g_ocv_compat = flags; }
+int sgmref_get_ocv_compat(void) { return g_ocv_compat; }
+static inline int16_t adds16(int a, int b) { return sat16(a + b); }   /* _mm_adds_epi16 */
+static inline int16_t subs16(int a, int b) { return sat16(a - b); }   /* _mm_subs_epi16 */
+
 /* Effective parameters: head of OpenCV computeDisparitySGBM. */
 typedef struct {
     int minD, maxD, D;
@@ -50,6 +84,7 @@ typedef struct {
     int invalid_scaled;
     int subpix, lr, median, census;
     int npasses;
+    int compat;          /* SGMREF_OCV_* bits (OCV modes only) */
 } eff_t;
 
 int sgmref_effective(const sgm_params* p, int width, int height, int* out /* 16 ints */);
@@ -84,6 +119,7 @@ static int effective(const sgm_params* p, int width, int height, eff_t* e)
         e->subpix = 1; e->lr = 1; e->median = 1;
         e->npasses = p->mode == SGM_MODE_OCV_HH8 ? 2 : 1;
     }
+    e->compat = e->census ? 0 : g_ocv_compat;
     e->uniq = p->uniqueness_ratio >= 0 ? p->uniqueness_ratio : 10;
     e->disp12 = p->disp12_max_diff > 0 ? p->disp12_max_diff : 1;
     e->minX1 = imax(e->maxD, 0);
@@ -215,8 +251,20 @@ static void wta_pixel(const eff_t* e, int x, const int* Sp, int16_t* disp_row, w
 {
     const int D = e->D;
     int minS = MAX_COST, bestDisp = -1, d;
-    for (d = 0; d < D; d++)
-        if (Sp[d] < minS) { minS = Sp[d]; bestDisp = d; }
+    if ((e->compat & SGMREF_OCV_LANE_TIE) && e->npasses == 1) {
+        /* SSE2: lane l (d = l, l+8, ...) keeps its first strict minimum from MAX_COST; the
+         * lowest lane holding the overall minimum wins (LSBTab) */
+        int lmin[8], lbest[8];
+        for (int l = 0; l < 8; l++) { lmin[l] = MAX_COST; lbest[l] = -1; }
+        for (d = 0; d < D; d++)
+            if (Sp[d] < lmin[d & 7]) { lmin[d & 7] = Sp[d]; lbest[d & 7] = d; }
+        for (int l = 0; l < 8; l++) minS = imin(minS, lmin[l]);
+        for (int l = 0; l < 8; l++)
+            if (lmin[l] == minS) { bestDisp = lbest[l]; break; }
+    } else {
+        for (d = 0; d < D; d++)
+            if (Sp[d] < minS) { minS = Sp[d]; bestDisp = d; }
+    }
     for (d = 0; d < D; d++)
         if (Sp[d] * (100 - e->uniq) < minS * 100 && abs(bestDisp - d) > 1) break;
     if (d < D) return;                         /* uniqueness reject: no disp2 update either */
@@ -379,16 +427,25 @@ static int ocv_cost_rows(const uint8_t* L, const uint8_t* R, int w, int h, size_
                     for (int x = 1; x <= SW2; x++) s += pixDiff[(size_t)imin(x, width1 - 1) * D + d];
                     hsumAdd[d] = (int16_t)s;
                 }
+                /* CV_SIMD saturates the running sums of rows y > 0 (the y == 0 rows run the
+                 * scalar loop in every version) */
+                const int sat = (e->compat & SGMREF_OCV_SIMD_SAT) && y > 0;
                 for (int x = 1; x < width1; x++) {
                     const int16_t* pixAdd = pixDiff + (size_t)imin(x + SW2, width1 - 1) * D;
                     const int16_t* pixSub = pixDiff + (size_t)imax(x - SW2 - 1, 0) * D;
+                    int16_t* hx = hsumAdd + (size_t)x * D;
+                    const int16_t* hp = hsumAdd + (size_t)(x - 1) * D;
                     for (int d = 0; d < D; d++)
-                        hsumAdd[(size_t)x * D + d] = (int16_t)(hsumAdd[(size_t)(x - 1) * D + d] + pixAdd[d] - pixSub[d]);
+                        hx[d] = sat ? adds16(subs16(hp[d], pixSub[d]), pixAdd[d])
+                                    : (int16_t)(hp[d] + pixAdd[d] - pixSub[d]);
                 }
                 if (y > 0) {
                     const int16_t* hsumSub = hsumBuf + (size_t)(imax(y - SH2 - 1, 0) % hsumBufNRows) * costBufSize;
-                    for (size_t i = 0; i < costBufSize; i++)
-                        C[i] = (int16_t)(Cprev[i] + hsumAdd[i] - hsumSub[i]);
+                    /* 3.x: the vertical update starts at column 1 (x = D) */
+                    const size_t i0 = (e->compat & SGMREF_OCV_COL0_LEGACY) ? (size_t)D : 0;
+                    for (size_t i = i0; i < costBufSize; i++)
+                        C[i] = sat ? adds16(subs16(Cprev[i], hsumSub[i]), hsumAdd[i])
+                                   : (int16_t)(Cprev[i] + hsumAdd[i] - hsumSub[i]);
                 }
             }
             if (y == 0) {
@@ -490,18 +547,35 @@ static int ocv_match(const eff_t* e, const uint8_t* L, const uint8_t* R, int w, 
                 const int16_t* Cp = C + (size_t)x * D;
                 uint16_t* Sp = S + (size_t)x * D;
                 int minL0 = MAX_COST, minL1 = MAX_COST, minL2 = MAX_COST, minL3 = MAX_COST;
-                for (int d = 0; d < D; d++) {
-                    int Cpd = Cp[d];
-                    int L0 = Cpd + imin(Lp0[d], imin(Lp0[d - 1] + P1, imin(Lp0[d + 1] + P1, delta0))) - delta0;
-                    int L1 = Cpd + imin(Lp1[d], imin(Lp1[d - 1] + P1, imin(Lp1[d + 1] + P1, delta1))) - delta1;
-                    int L2 = Cpd + imin(Lp2[d], imin(Lp2[d - 1] + P1, imin(Lp2[d + 1] + P1, delta2))) - delta2;
-                    int L3 = Cpd + imin(Lp3[d], imin(Lp3[d - 1] + P1, imin(Lp3[d + 1] + P1, delta3))) - delta3;
-                    /* Lr rows are CostType (int16) in OpenCV */
-                    LR(Lr[0], x, 0)[d] = (int16_t)L0; minL0 = imin(minL0, L0);
-                    LR(Lr[0], x, 1)[d] = (int16_t)L1; minL1 = imin(minL1, L1);
-                    LR(Lr[0], x, 2)[d] = (int16_t)L2; minL2 = imin(minL2, L2);
-                    LR(Lr[0], x, 3)[d] = (int16_t)L3; minL3 = imin(minL3, L3);
-                    Sp[d] = (uint16_t)sat16((int)(int16_t)Sp[d] + L0 + L1 + L2 + L3);
+                if (e->compat & SGMREF_OCV_SIMD_SAT) {
+                    /* _delta = v_setall_s16((short)delta): the int sum wraps to int16 */
+                    const int dl0 = (int16_t)delta0, dl1 = (int16_t)delta1, dl2 = (int16_t)delta2, dl3 = (int16_t)delta3;
+                    for (int d = 0; d < D; d++) {
+                        int Cpd = Cp[d];
+                        int L0 = adds16(subs16(imin(imin(Lp0[d], adds16(Lp0[d - 1], P1)), imin(adds16(Lp0[d + 1], P1), dl0)), dl0), Cpd);
+                        int L1 = adds16(subs16(imin(imin(Lp1[d], adds16(Lp1[d - 1], P1)), imin(adds16(Lp1[d + 1], P1), dl1)), dl1), Cpd);
+                        int L2 = adds16(subs16(imin(imin(Lp2[d], adds16(Lp2[d - 1], P1)), imin(adds16(Lp2[d + 1], P1), dl2)), dl2), Cpd);
+                        int L3 = adds16(subs16(imin(imin(Lp3[d], adds16(Lp3[d - 1], P1)), imin(adds16(Lp3[d + 1], P1), dl3)), dl3), Cpd);
+                        LR(Lr[0], x, 0)[d] = L0; minL0 = imin(minL0, L0);
+                        LR(Lr[0], x, 1)[d] = L1; minL1 = imin(minL1, L1);
+                        LR(Lr[0], x, 2)[d] = L2; minL2 = imin(minL2, L2);
+                        LR(Lr[0], x, 3)[d] = L3; minL3 = imin(minL3, L3);
+                        Sp[d] = (uint16_t)adds16(adds16((int16_t)Sp[d], adds16(L0, L1)), adds16(L2, L3));
+                    }
+                } else {
+                    for (int d = 0; d < D; d++) {
+                        int Cpd = Cp[d];
+                        int L0 = Cpd + imin(Lp0[d], imin(Lp0[d - 1] + P1, imin(Lp0[d + 1] + P1, delta0))) - delta0;
+                        int L1 = Cpd + imin(Lp1[d], imin(Lp1[d - 1] + P1, imin(Lp1[d + 1] + P1, delta1))) - delta1;
+                        int L2 = Cpd + imin(Lp2[d], imin(Lp2[d - 1] + P1, imin(Lp2[d + 1] + P1, delta2))) - delta2;
+                        int L3 = Cpd + imin(Lp3[d], imin(Lp3[d - 1] + P1, imin(Lp3[d + 1] + P1, delta3))) - delta3;
+                        /* Lr rows are CostType (int16) in OpenCV */
+                        LR(Lr[0], x, 0)[d] = (int16_t)L0; minL0 = imin(minL0, L0);
+                        LR(Lr[0], x, 1)[d] = (int16_t)L1; minL1 = imin(minL1, L1);
+                        LR(Lr[0], x, 2)[d] = (int16_t)L2; minL2 = imin(minL2, L2);
+                        LR(Lr[0], x, 3)[d] = (int16_t)L3; minL3 = imin(minL3, L3);
+                        Sp[d] = (uint16_t)sat16((int)(int16_t)Sp[d] + L0 + L1 + L2 + L3);
+                    }
                 }
                 MINLR(minLr[0], x, 0) = (int16_t)minL0; MINLR(minLr[0], x, 1) = (int16_t)minL1;
                 MINLR(minLr[0], x, 2) = (int16_t)minL2; MINLR(minLr[0], x, 3) = (int16_t)minL3;
@@ -517,7 +591,16 @@ static int ocv_match(const eff_t* e, const uint8_t* L, const uint8_t* R, int w, 
                         int* Lp0 = LR(Lr[0], x + 1, 0);
                         Lp0[-1] = Lp0[D] = MAX_COST;
                         const int16_t* Cp = C + (size_t)x * D;
+                        const int simd = (e->compat & SGMREF_OCV_SIMD_SAT) != 0;
+                        const int dl0 = (int16_t)delta0;
                         for (int d = 0; d < D; d++) {
+                            if (simd) {
+                                int L0 = adds16(subs16(imin(imin(Lp0[d], adds16(Lp0[d - 1], P1)), imin(adds16(Lp0[d + 1], P1), dl0)), dl0), Cp[d]);
+                                LR(Lr[0], x, 0)[d] = L0;
+                                minL0 = imin(minL0, L0);
+                                Sp[d] = (uint16_t)adds16(L0, (int16_t)Sp[d]);
+                                continue;
+                            }
                             int L0 = Cp[d] + imin(Lp0[d], imin(Lp0[d - 1] + P1, imin(Lp0[d + 1] + P1, delta0))) - delta0;
                             LR(Lr[0], x, 0)[d] = (int16_t)L0;
                             minL0 = imin(minL0, L0);

@@ -87,6 +87,8 @@ def lib():
         L.sgmref_filter_speckles.argtypes = [i16p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.sgmref_effective.argtypes = [P(SgmParams), ctypes.c_int, ctypes.c_int, P(ctypes.c_int)]
+        L.sgmref_set_ocv_compat.argtypes = [ctypes.c_int]
+        L.sgmref_get_ocv_compat.restype = ctypes.c_int
         L.sgmref_num_threads.restype = ctypes.c_int
         L.sgmref_set_num_threads.argtypes = [ctypes.c_int]
         _lib = L
@@ -178,6 +180,28 @@ def filter_speckles(disp, new_val, max_size, max_diff):
     h, w = d.shape
     _check(lib().sgmref_filter_speckles(_ptr(d), w, h, w, new_val, max_size, max_diff), "speckles")
     return d
+
+
+# OpenCV build variants of the OCV modes (sgm_oracle.c); 0 = the default
+# restatement the GPU engine reproduces.
+OCV_COL0_LEGACY = 1    # 3.x: the vertical running sum skips C' column 0 for y > 0
+OCV_SIMD_SAT = 2       # CV_SIMD branches: int16 saturating sums / recurrence / S
+OCV_LANE_TIE = 4       # MODE_SGBM SSE2 WTA: lowest lane (d mod 8) wins among equal minima
+
+
+class ocv_compat:
+    """Context manager: run the oracle's OCV modes with the given SGMREF_OCV_* bits."""
+
+    def __init__(self, flags):
+        self.flags = int(flags)
+
+    def __enter__(self):
+        self.prev = int(lib().sgmref_get_ocv_compat())
+        lib().sgmref_set_ocv_compat(self.flags)
+        return self
+
+    def __exit__(self, *a):
+        lib().sgmref_set_ocv_compat(self.prev)
 
 
 def set_threads(n):
