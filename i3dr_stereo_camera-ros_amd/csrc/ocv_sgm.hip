@@ -192,6 +192,7 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
         for (int k = y - SH2; k <= y + SH2; k++) s += hs[(size_t)min(max(k, 0), H - 1) * rs + i];
         return s;
     };
+    bool ovf = false;                                      // a C' above int16 (Geom::wide == 2)
     const int ylast = max(H - SH2 - 1, 0);                 // last row whose window is recomputed
     const bool tail = y1 - 1 >= 1 && y1 - 1 + SH2 >= H;    // the segment reaches the repeated rows
     const int rep = fullDP ? g.P2 : g.P2 + (tail ? window(ylast) : 0);
@@ -219,8 +220,13 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
             } else {
                 v = rep;
             }
+            ovf |= v > kMaxCost;
             C[(size_t)y * rs + i] = (int16_t)v;
         }
+    }
+    if (g.wide == 2 && g.ovf) {                            // one atomic per wave that saw one
+        const uint64_t b = __ballot(ovf);
+        if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(g.ovf, 1);
     }
 }
 
@@ -447,6 +453,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
                                                   int4 nblk1, int use_buf)
 {
+    if (ocv_gate_skip<VT>(g)) return;
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
     // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
     int b = blockIdx.x, dir = 0, slot = 0;
@@ -568,6 +575,7 @@ template <int DPL, int NDIR, typename VT>
 __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, size_t vol_elems, Geom g,
                                                    int16_t* __restrict__ out, size_t out_stride)
 {
+    if (ocv_gate_skip<VT>(g)) return;
     extern __shared__ uint32_t lds_ocv[];
     int16_t* sl = (int16_t*)lds_ocv;                      // 16 lane rows x 16 lanes x DPL S values
     RowLds R((char*)lds_ocv + (size_t)16 * 16 * DPL * 2, g.W);
@@ -668,10 +676,11 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 
 // vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 VT of trash slots
 template <int DPL, int LPL, typename VT>
-static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t vol_elems, const Geom& g, int dirmask,
+static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, const Geom& g, int dirmask,
                                hipStream_t st)
 {
     VT* vols = (VT*)vols_;
+    const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     int ndir = 0;
     for (int i = 0; i < 8; i++) ndir += (dirmask >> i) & 1;
     const size_t trash_off = (size_t)ndir * vol_elems;
@@ -691,11 +700,12 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t vol_elems, 
 }
 
 template <int DPL, int LPL>
-static void launch_ocv_paths_v(const int16_t* C, void* vols, size_t vol_elems, const Geom& g, int dirmask,
+static void launch_ocv_paths_v(const int16_t* C, void* vols, size_t cells, const Geom& g, int dirmask,
                                hipStream_t st)
 {
-    if (g.wide) launch_ocv_paths_l<DPL, LPL, int32_t>(C, vols, vol_elems, g, dirmask, st);
-    else launch_ocv_paths_l<DPL, LPL, int16_t>(C, vols, vol_elems, g, dirmask, st);
+    // gated (wide == 2): both launches, the one not matching *g.ovf exits at once
+    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t>(C, vols, cells, g, dirmask, st);
+    if (g.wide != 0) launch_ocv_paths_l<DPL, LPL, int32_t>(C, vols, cells, g, dirmask, st);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
@@ -716,32 +726,33 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
     return waves < kOcvWideLineWaves ? 32 : 16;
 }
 
-hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t vol_elems, const Geom& g, int dirmask,
+hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t cells, const Geom& g, int dirmask,
                             hipStream_t st)
 {
     const int D = g.D;
     if (ocv_lanes_per_line(g, dirmask) == 32) {
-        if (D <= 64) launch_ocv_paths_v<2, 32>(C, vols, vol_elems, g, dirmask, st);
-        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, vols, vol_elems, g, dirmask, st);
-        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, vols, vol_elems, g, dirmask, st);
-        else launch_ocv_paths_v<16, 32>(C, vols, vol_elems, g, dirmask, st);
+        if (D <= 64) launch_ocv_paths_v<2, 32>(C, vols, cells, g, dirmask, st);
+        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, vols, cells, g, dirmask, st);
+        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<16, 32>(C, vols, cells, g, dirmask, st);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_v<1, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 2: launch_ocv_paths_v<2, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 4: launch_ocv_paths_v<4, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 8: launch_ocv_paths_v<8, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        case 16: launch_ocv_paths_v<16, 16>(C, vols, vol_elems, g, dirmask, st); break;
-        default: launch_ocv_paths_v<32, 16>(C, vols, vol_elems, g, dirmask, st); break;
+        case 1: launch_ocv_paths_v<1, 16>(C, vols, cells, g, dirmask, st); break;
+        case 2: launch_ocv_paths_v<2, 16>(C, vols, cells, g, dirmask, st); break;
+        case 4: launch_ocv_paths_v<4, 16>(C, vols, cells, g, dirmask, st); break;
+        case 8: launch_ocv_paths_v<8, 16>(C, vols, cells, g, dirmask, st); break;
+        case 16: launch_ocv_paths_v<16, 16>(C, vols, cells, g, dirmask, st); break;
+        default: launch_ocv_paths_v<32, 16>(C, vols, cells, g, dirmask, st); break;
         }
     }
     return hipGetLastError();
 }
 
 template <int DPL, typename VT>
-static void launch_ocv_wta_dpl(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+static void launch_ocv_wta_dpl(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                                size_t out_stride, hipStream_t st)
 {
+    const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
     const VT* v = (const VT*)vols;
     if (ndir == 8)
@@ -751,23 +762,24 @@ static void launch_ocv_wta_dpl(const void* vols, size_t vol_elems, int ndir, con
 }
 
 template <typename VT>
-static void launch_ocv_wta_t(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                              size_t out_stride, hipStream_t st)
 {
     const int D = g.D;
-    if (D <= 32) launch_ocv_wta_dpl<2, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 64) launch_ocv_wta_dpl<4, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 128) launch_ocv_wta_dpl<8, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else if (D <= 256) launch_ocv_wta_dpl<16, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_dpl<32, VT>(vols, vol_elems, ndir, g, out, out_stride, st);
+    if (D <= 32) launch_ocv_wta_dpl<2, VT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 64) launch_ocv_wta_dpl<4, VT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 128) launch_ocv_wta_dpl<8, VT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 256) launch_ocv_wta_dpl<16, VT>(vols, cells, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_dpl<32, VT>(vols, cells, ndir, g, out, out_stride, st);
 }
 
-// vols: int16 volumes, or int32 when g.wide (see ocv_volume_bytes)
-hipError_t launch_ocv_wta(const void* vols, size_t vol_elems, int ndir, const Geom& g, int16_t* out,
+// vols: int16 volumes (wide 0), int32 (wide 1), or an int32-sized region read as the one
+// the cost kernel's overflow flag selects (wide 2); cells = width1 * H * D per volume
+hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                           size_t out_stride, hipStream_t st)
 {
-    if (g.wide) launch_ocv_wta_t<int32_t>(vols, vol_elems, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_t<int16_t>(vols, vol_elems, ndir, g, out, out_stride, st);
+    if (g.wide != 1) launch_ocv_wta_t<int16_t>(vols, cells, ndir, g, out, out_stride, st);
+    if (g.wide != 0) launch_ocv_wta_t<int32_t>(vols, cells, ndir, g, out, out_stride, st);
     return hipGetLastError();
 }
 

@@ -91,9 +91,16 @@ int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
         // C = box sum + P2 stays in int16 below this bound, and then every path cost lies in
         // [C - P2, C]: int16 volumes are exact. Above it C may wrap (OpenCV's CostType) and a
         // path cost can leave int16, while OpenCV adds the int value into S: int32 volumes.
+        // When the bound allows it, the cost kernel flags the C' values that do leave int16 and
+        // only frames with such a value take the int32 volumes (Geom::wide == 2): real images
+        // stay far below the bound (the reference launch config, block 21: bound 41 413).
+        // SGM_OCV_WIDE=1 forces int32 volumes; SGM_OCV_GATE=0 takes them whenever the bound allows.
         const long long cmax = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63) + g.P2;
         const char* wide_env = std::getenv("SGM_OCV_WIDE");
-        g.wide = cmax > 32767 || (wide_env && std::atoi(wide_env) != 0);
+        const char* gate_env = std::getenv("SGM_OCV_GATE");
+        if (wide_env && std::atoi(wide_env) != 0) g.wide = 1;
+        else if (cmax > 32767) g.wide = (gate_env && std::atoi(gate_env) == 0) ? 1 : 2;
+        else g.wide = 0;
     }
     g.uniq = p.uniqueness_ratio >= 0 ? p.uniqueness_ratio : 10;
     g.disp12 = p.disp12_max_diff > 0 ? p.disp12_max_diff : 1;
@@ -280,7 +287,7 @@ struct Layout {
     size_t vol_bytes = 0;
     int group = 1;                                         // frames per pipelined launch
     size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
-    size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovol_elems = 0;  // ocv
+    size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0;                      // host-API staging
     size_t total = 0;
@@ -316,10 +323,11 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
         const size_t es = g.wide ? 4 : 2;          // int32 / int16 path volumes (Geom::wide)
-        l.ovol_elems = align_up(cells * es) / es;
         // + slack: the path kernel's trash slots (64 lanes x 32 values) and the WTA's last pixel
         // group of the last row, which reads 3 pixels past the volume
-        l.ovols = take(es * (l.ovol_elems * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 64 * 32 + (size_t)8 * g.D));
+        l.ovols = take(es * (sgm::ocv_vol_elems(cells, es) * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 64 * 32 +
+                             (size_t)8 * g.D));
+        l.ovf = take(sizeof(int));
     }
     l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
@@ -448,12 +456,19 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         int16_t* A = (int16_t*)(ws + l.bufA);
         int16_t* B = (int16_t*)(ws + l.bufB);
         void* V = ws + l.ovols;
+        const size_t ncells = (size_t)g.width1 * g.H * g.D;
+        Geom gg = g;
+        if (g.wide == 2) {             // the cost kernel raises the flag, the gated launches read it
+            gg.ovf = (int*)(ws + l.ovf);
+            HIP_TRY(hipMemsetAsync(gg.ovf, 0, sizeof(int), st), "hipMemsetAsync");
+        }
+        const double es = g.wide == 1 ? 4 : 2;   // gated: the int16 case (real images)
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
-        HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, g, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
-        rec.begin("ocv_paths", 2 * cells * (ndir + 1));
-        HIP_TRY(sgm::launch_ocv_paths(A, V, l.ovol_elems, g, mask, st), "ocv_paths");
-        rec.begin("ocv_wta_lr", 2 * cells * ndir + 2 * WH);
-        HIP_TRY(sgm::launch_ocv_wta(V, l.ovol_elems, ndir, g, dst, dst_stride, st), "ocv_wta");
+        HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, gg, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
+        rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
+        HIP_TRY(sgm::launch_ocv_paths(A, V, ncells, gg, mask, st), "ocv_paths");
+        rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
+        HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
     }
     int rc = run_post(h, l, g, dOut, out_stride, rec);
     if (rc) return rc;
@@ -604,7 +619,6 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     int rc = make_geom(h->params, W, H, g, h->err);
     if (rc) return rc;
     if ((rc = ensure_stream(h))) return rc;
-    if ((rc = order_after_last(h, h->stream))) return rc;   // synchronous calls run on the handle's stream
     l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
     if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
@@ -914,7 +928,7 @@ int sgm_match(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, s
     Geom g;
     Layout l;
     int rc = prepare(h, W, H, true, g, l);
-    if (rc) return rc;
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
     const size_t WH = (size_t)W * H;
     if ((rc = ensure_pin(h, WH * 4))) return rc;
     char* ws = (char*)h->ws.base;
@@ -1205,6 +1219,7 @@ int stream_host_frames(sgm_handle* h, const uint8_t* const* lefts, const uint8_t
     const bool pipelined = h->params.mode == SGM_MODE_CENSUS8 && n >= 2 && g.width1 > 0;
     Layout l;
     if ((rc = prepare(h, W, H, false, g, l, pipelined ? batch_group(n) : 0))) return rc;
+    if ((rc = order_after_last(h, h->stream))) return rc;
     const size_t WH = (size_t)W * H;
     if ((rc = ensure_io(h, WH))) return rc;
     HostStreamer s;
@@ -1679,7 +1694,7 @@ int sgm_debug_census_path(sgm_handle* h, const uint8_t* L, const uint8_t* R, int
     Geom g;
     Layout l;
     int rc = prepare(h, W, H, true, g, l);
-    if (rc) return rc;
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
     if (g.width1 <= 0) return SGM_OK;
     char* ws = (char*)h->ws.base;
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -1709,7 +1724,7 @@ int sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W,
     Geom g;
     Layout l;
     int rc = prepare(h, W, H, true, g, l);
-    if (rc) return rc;
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
     if (g.width1 <= 0) return SGM_OK;
     char* ws = (char*)h->ws.base;
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");

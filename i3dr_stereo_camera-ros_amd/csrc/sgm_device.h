@@ -38,8 +38,22 @@ struct Geom {
     int subpix, lr;         // census: subpixel / LR-check flags (OCV: 1, 1)
     int invalid;            // (minD - 1) * 16
     int SW2, SH2, ftzero;   // OCV: SAD half window, prefilter cap
-    int wide;               // OCV: a cost may leave int16 -> int32 path volumes (exact S)
+    int wide;               // OCV path volumes: 0 int16; 1 int32 (a cost may leave int16: exact S);
+                            // 2 gated: the cost kernel sets *ovf when a C' actually leaves
+                            // int16, and int16 / int32 launches each run only on their case
+    int* ovf;               // device flag of wide == 2 (null otherwise)
 };
+
+// Elements of one OCV path volume of `cells` cells at es bytes per cell (256-B aligned
+// slices; the host layout and the kernels' launchers agree on it).
+__host__ __device__ inline size_t ocv_vol_elems(size_t cells, size_t es) { return (cells * es + 255) / 256 * 256 / es; }
+// Gate of the wide == 2 launches: false when this launch's element type is not the one the
+// frame needs (uniform: a kernel argument and one scalar load).
+template <typename VT>
+__device__ __forceinline__ bool ocv_gate_skip(const Geom& g)
+{
+    return g.wide == 2 && ((*g.ovf != 0) != (sizeof(VT) == 4));
+}
 
 // Direction r = (rx, ry): L_r(p) depends on L_r(p - r). Engine volume order.
 __host__ __device__ constexpr int dir_rx(int i) { return i == 2 || i == 4 || i == 6 ? 1 : (i == 3 || i == 5 || i == 7 ? -1 : 0); }

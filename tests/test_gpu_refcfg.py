@@ -1,0 +1,88 @@
+"""The reference's own shipped SGBM configuration on the GPU (VERDICT r1 "missing" #2).
+
+launch/stereo_matcher.launch:37-48 (stereo_algorithm 1 = OpenCV SGBM): min_disparity 147,
+disparity_range 480, correlation_window_size 21, uniqueness_ratio 2, speckle 1000 / 4,
+prefilter_cap 7, P1 200, P2 400; capture size 2448 x 2048 (launch/stereo_capture.launch:14-15).
+The setters reach cv::StereoSGBM unchanged (matcherOpenCVSGBM.cpp:53-110, via
+generate_disparity.cpp:241-261). With a 21 x 21 box at ftzero 15 a cost may leave int16
+(bound 441 * 93 + 400 = 41 413), so the engine runs gated: the cost kernel flags the C'
+values that do, and only then do the int32 volumes run (Geom::wide == 2).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import to_oracle_params
+
+pytestmark = pytest.mark.gpu
+
+REF_W, REF_H = 2448, 2048
+REF_KW = dict(min_disparity=147, num_disparities=480, block_size=21, uniqueness_ratio=2, speckle_window_size=1000,
+              speckle_range=4, prefilter_cap=7, p1=200, p2=400)
+
+
+def _params(pkg, mode):
+    return pkg.default_params(pkg.MODE_OCV_SGBM5 if mode == "sgbm" else pkg.MODE_OCV_HH8, **REF_KW)
+
+
+@pytest.fixture(scope="module")
+def ref_frame(synth):
+    return synth.stereo_pair(REF_H, REF_W, 147, 480, seed=2448)
+
+
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_reference_config_full_width_crop_vs_oracle(engine, oracle, pkg, ref_frame, mode, monkeypatch):
+    """A full-width 2448 x 160 crop of the capture-size frame: bit-exact vs the oracle, in the
+    gated mode (no C' leaves int16 on this image: int16 volumes) and with the int32 volumes
+    forced (SGM_OCV_GATE=0, the static choice)."""
+    left, right, _ = ref_frame
+    l, r = np.ascontiguousarray(left[600:760]), np.ascontiguousarray(right[600:760])
+    p = _params(pkg, mode)
+    engine.set_params(p)
+    ref = oracle.match(to_oracle_params(oracle, p), l, r)
+    got = engine.match(l, r)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    monkeypatch.setenv("SGM_OCV_GATE", "0")
+    got32 = engine.match(l, r)
+    assert np.array_equal(got32, ref), f"int32 volumes: {(got32 != ref).sum()} pixels differ"
+    assert (ref != (147 - 1) * 16).mean() > 0.3          # the crop is mostly matched
+
+
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_reference_config_gate_takes_int32_on_overflow(engine, oracle, pkg, mode):
+    """Same box and P2, a frame whose costs do leave int16 (binary noise against its negative at
+    preFilterCap 63): the flag routes it to the int32 volumes, bit-exact vs the oracle (an int16
+    path would differ)."""
+    rng = np.random.default_rng(1)
+    left = (rng.integers(0, 2, (64, 900)) * 255).astype(np.uint8)
+    right = 255 - left
+    p = pkg.default_params(pkg.MODE_OCV_SGBM5 if mode == "sgbm" else pkg.MODE_OCV_HH8,
+                           **dict(REF_KW, prefilter_cap=63, speckle_window_size=0))
+    engine.set_params(p)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    got = engine.match(left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_reference_config_full_frame_properties(engine, pkg, ref_frame, mode, monkeypatch):
+    """The whole 2448 x 2048 frame (the CPU oracle takes minutes at this size): repeatable,
+    identical through the gated int16 and the forced int32 volumes, inside the search window
+    and close to the synthetic truth."""
+    left, right, truth = ref_frame
+    p = _params(pkg, mode)
+    engine.set_params(p)
+    a = engine.match(left, right)
+    b = engine.match(left, right)
+    assert np.array_equal(a, b)
+    monkeypatch.setenv("SGM_OCV_GATE", "0")
+    c = engine.match(left, right)
+    assert np.array_equal(a, c), f"gated vs int32 volumes: {(a != c).sum()} pixels differ"
+    valid = a != (147 - 1) * 16
+    assert valid.mean() > 0.5
+    err = np.abs(a[valid] / 16.0 - truth[valid])
+    assert np.median(err) < 0.5 and (err < 2).mean() > 0.9, (np.median(err), (err < 2).mean())
+    # disparities inside the search window
+    v = a[valid]
+    assert v.min() >= 147 * 16 and v.max() <= (147 + 480) * 16
