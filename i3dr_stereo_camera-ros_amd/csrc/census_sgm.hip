@@ -20,6 +20,13 @@
 #ifndef SGM_NT_LOAD
 #define SGM_NT_LOAD 1      // WTA volume loads with the nt cache policy (0: default)
 #endif
+#ifndef SGM_EXP
+#define SGM_EXP 0          // timing-only experiments (results invalid): bit 0 row segments from row 0,
+                           // bit 1 dir-1 volume stores to the trash slot, bit 2 WTA reads 7 volumes
+#endif
+#ifndef SGM_UPWTA_PRIO
+#define SGM_UPWTA_PRIO 0   // s_setprio of the up+WTA blocks (0: default priority)
+#endif
 #ifndef SGM_ROWS_LPL8
 #define SGM_ROWS_LPL8 0    // 1: row sweeps with 8 lanes per path line for D <= 256 (RowsCfg; measured slower)
 #endif
@@ -431,7 +438,7 @@ __device__ __forceinline__ void seg_load(SegRegs<DPL, LPL>& v, const SegAddr<DPL
                                          const Geom& g, int rx, int ry, int xb, int s)
 {
     const int y = ry > 0 ? s : g.H - 1 - s;
-    const int yc = min(max(y, 0), g.H - 1);
+    const int yc = (SGM_EXP & 1) ? 0 : min(max(y, 0), g.H - 1);
     const char* sb = a.lo + (size_t)8 * ((size_t)yc * g.W + (xb + rx * s));   // wave-uniform
 #pragma unroll
     for (int m = 0; m < RowSeg<DPL, LPL>::NLOAD; m++) v[m] = *(const uint64_t*)(sb + a.off[m]);
@@ -466,13 +473,36 @@ __device__ __forceinline__ void p16_seed(const uint8_t* src, const uint32_t (&im
     p16_relative<DPL, LPL>(Labs, Lr);
 }
 
+// The last sweep fused with the WTA (census_fused16 "up+WTA" blocks): the upward vertical
+// sweep (dir 1) of a frame whose other seven volumes are complete; at each step every line
+// holds L_1(x, y, .) in the WTA's 16-lanes-per-pixel layout, adds the seven stored costs of
+// (x, y) and runs the WTA of that pixel, so volume 1 is never written or read. The per-pixel
+// results (d16 | best << 16 | minS << 32; rejected: d16 = invalid, best = -1) go to res[y][x];
+// k_census_rowfin does disp2 + LR of each row from them.
+struct UpWta {
+    const uint8_t* vols;     // the frame's volume set: direction v at vols + v * vol_bytes
+    size_t vol_bytes;
+    uint64_t* res;           // [H][W] results + 64 trash slots
+};
+struct WtaPix { int best, minS, d16; bool rej; };   // one pixel's WTA result (wta_pix16)
+template <int DPL, bool EXACT>
+__device__ __forceinline__ WtaPix wta_pix16(const uint32_t (&E)[(DPL + 3) / 4], const uint32_t (&O)[(DPL + 3) / 4],
+                                            int p, const Geom& g, float inv_u, uint32_t* srow);
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void wta_emask(int p, const Geom& g, uint32_t (&emaskE)[(DPL + 3) / 4],
+                                          uint32_t (&emaskO)[(DPL + 3) / 4]);
+// LDS of an up+WTA block: the row sweep's code buffers, then 16 lines x 32 x NWD S dwords
+template <int DPL>
+__host__ __device__ constexpr size_t upwta_lds_bytes() { return (size_t)8 * 2 * RowSeg<DPL, 16>::BUF + (size_t)16 * 32 * ((DPL + 3) / 4) * 4; }
+
 // NL lines of direction dir starting at base column xb (DPL disparities per lane, LPL
 // lanes per line; lds: 2 * RowSeg<DPL, LPL>::BUF codes).
-template <int DPL, bool EXACT, int LPL>
+template <int DPL, bool EXACT, int LPL, bool FUSE = false>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
-                                         int xb, const PathLaunch16& pl, uint64_t* lds)
+                                         int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{})
 {
+    static_assert(!FUSE || LPL == 16, "up+WTA blocks use 16 lanes per line (the WTA layout)");
     using RS = RowSeg<DPL, LPL>;
     constexpr int M = DPL / 2;
     constexpr int NL = RS::NL;
@@ -526,20 +556,71 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     seg_load<DPL, LPL>(R3, sa, g, rx, ry, xb, min(s0 + 3, s1 - 1));
     __syncthreads();
 
+    // up+WTA (FUSE): the seven other volumes of the line's pixel, loaded one step ahead
+    constexpr int NWD = (DPL + 3) / 4;
+    uint32_t vw[7][NWD], emaskE[NWD], emaskO[NWD];
+    uint32_t* srow = (uint32_t*)(lds + 2 * RS::BUF) + j * 32 * NWD;
+    const float inv_u = 1.0f / (float)max(100 - g.uniq, 1);
+    const uint32_t voff = (uint32_t)((min(max(xb + j, g.minX1), g.maxX1 - 1) - g.minX1) * g.D + (lane_act ? p * DPL : 0));
+    auto vload = [&](int s) {
+        const uint8_t* rb = uw.vols + (size_t)max(g.H - 1 - s, 0) * g.width1 * g.D;   // wave-uniform
+#pragma unroll
+        for (int k = 0; k < 7; k++) wload_buf<DPL>(rb + (size_t)(k == 0 ? 0 : k + 1) * uw.vol_bytes, voff, vw[k]);
+    };
+    if constexpr (FUSE) {
+        wta_emask<DPL, EXACT>(p, g, emaskE, emaskO);
+        vload(s0);
+    }
     auto step = [&](int s, const uint64_t* bufc) {
         const int x = xb + j + rx * s;
         const bool valid = s < s1 && x >= g.minX1 && x < g.maxX1;
         const int y = ry > 0 ? s : g.H - 1 - s;
         const uint64_t cl = bufc[RS::NPAD + j];
         uint32_t Labs[M];
+        uint32_t E[NWD], O[NWD];
+        if constexpr (FUSE) {       // this step's seven costs, then the next step's loads
+#pragma unroll
+            for (int jj = 0; jj < NWD; jj++) {
+                uint32_t e = 0, o = 0;
+#pragma unroll
+                for (int k = 0; k < 7; k++) {
+                    e += vw[k][jj] & 0x00FF00FFu;
+                    o += __builtin_amdgcn_perm(0u, vw[k][jj], 0x0c030c01u);
+                }
+                asm("" : "+v"(e), "+v"(o));     // the sums, not 14 extracted words, stay live
+                E[jj] = e;
+                O[jj] = o;
+            }
+        }
         // path start (first valid pixel of the line): L = C. The P2 cap of the recurrence is
         // lowered to "0" (kBase), which clamps every candidate: one select per step.
         const uint32_t P2x = pv ? P2P2 : kBaseP2;
+        if constexpr (FUSE) __builtin_amdgcn_sched_barrier(0);
         p16_step<DPL, EXACT, LPL>(Lr, cl, [&](int k) { return bufc[RS::phys(e_hi - k)]; }, P1P1, P2x, imask, Labs);
-        const bool ok = valid && lane_act;
-        uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
-        uint8_t* const dst = ok ? vrow + (uint32_t)((x - g.minX1) * g.D + p * DPL) : tr;
-        store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
+        if constexpr (FUSE) {
+            __builtin_amdgcn_sched_barrier(0);
+            // + L_1: the low byte of each biased-f16 pattern (pair i holds d = 2i, 2i + 1)
+#pragma unroll
+            for (int jj = 0; jj < NWD; jj++) {
+                const uint32_t a = Labs[2 * jj], b = 2 * jj + 1 < M ? Labs[2 * jj + 1] : 0u;
+                E[jj] = (E[jj] + __builtin_amdgcn_perm(b, a, 0x0c040c00u)) | emaskE[jj];
+                O[jj] = (O[jj] + __builtin_amdgcn_perm(b, a, 0x0c060c02u)) | emaskO[jj];
+            }
+            // the next step's loads: in flight during this step's WTA (not during the sweep step,
+            // whose temporaries they would otherwise share the register file with)
+            vload(s + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const WtaPix px = wta_pix16<DPL, EXACT>(E, O, p, g, inv_u, srow);
+            const uint64_t v = (uint64_t)(uint16_t)(px.rej ? g.invalid : px.d16) |
+                               ((uint64_t)(uint16_t)(px.rej ? -1 : px.best) << 16) | ((uint64_t)(uint16_t)px.minS << 32);
+            uint64_t* dst = (valid && p == 0) ? uw.res + (size_t)y * g.W + x : uw.res + (size_t)g.W * g.H + lane;
+            __builtin_nontemporal_store(v, dst);
+        } else {
+            const bool ok = valid && lane_act && !((SGM_EXP & 2) && dir == 1);
+            uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
+            uint8_t* const dst = ok ? vrow + (uint32_t)((x - g.minX1) * g.D + p * DPL) : tr;
+            store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
+        }
         pv = valid;
     };
     // step s reads buf[s & 1] (holding segment s), then segment s + 1 (register set
@@ -572,7 +653,7 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     const int dir = (int)(it >> 24);
     const int f = (int)((it >> 22) & 3u);
     const int lb = (int)(it & 0x3FFFFFu);
-    if (f >= pf.n) return;                          // uniform over the workgroup
+    if (f >= pf.n || ((pf.skip_dirs >> dir) & 1u)) return;    // uniform over the workgroup
     const uint64_t* cL = pick4(pf.cL, f);
     const uint64_t* cR = pick4(pf.cR, f);
     uint8_t* V = pick4(pf.vols, f) + (size_t)dir * vol_bytes;
@@ -628,6 +709,89 @@ __host__ __device__ constexpr size_t wta_key_bytes(int W)
 template <int DPL>
 __host__ __device__ constexpr size_t wta_lds_bytes(int W) { return wta_key_bytes<DPL>(W) + RowLds::rest_bytes(W); }
 
+// WTA of the 4 pixels a wave holds (one per 16-lane row, lane p: d = p*DPL ..), from their
+// S in packed u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]); halves past D or
+// past the lane's DPL hold 0xFFFF. srow: the row's LDS slice (16 lanes x 2 * NWD dwords).
+template <int DPL, bool EXACT>
+__device__ __forceinline__ WtaPix wta_pix16(const uint32_t (&E)[(DPL + 3) / 4], const uint32_t (&O)[(DPL + 3) / 4],
+                                            int p, const Geom& g, float inv_u, uint32_t* srow)
+{
+    constexpr int NWD = (DPL + 3) / 4;
+    // packed-key geometry: lane-local index k in the low KB bits of a 16-bit key
+    constexpr int KB = DPL > 16 ? 5 : 4;
+    constexpr uint32_t KMASK = (1u << KB) - 1;
+    // ---- (minS, best): packed 16-bit keys S << KB | k, one 16-lane min over S*512 + d ----
+    uint32_t km = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < NWD; j++) {
+        const uint32_t ke = pk_shl(E[j], KB) | (((uint32_t)(4 * j + 2) << 16) | (uint32_t)(4 * j));
+        const uint32_t ko = pk_shl(O[j], KB) | (((uint32_t)(4 * j + 3) << 16) | (uint32_t)(4 * j + 1));
+        km = pk_min(km, pk_min(ke, ko));
+    }
+    km = pk_min(km, alignbit16(km, km)) & 0xFFFFu;      // lane min key (low half)
+    const uint32_t kmin = row_min_u32(((km >> KB) << 9) | (uint32_t)(p * DPL + (int)(km & KMASK)));
+    WtaPix r;
+    const int best = (int)(kmin & 511u);
+    const int minS = (int)(kmin >> 9);
+    // ---- the row's packed S slice in LDS (S[best +- 1] for subpixel and uniqueness) ----
+#pragma unroll
+    for (int j = 0; j < NWD; j++) { srow[p * 2 * NWD + j] = E[j]; srow[p * 2 * NWD + NWD + j] = O[j]; }
+    auto s_at = [&](int d) {
+        const int kk = d % DPL;
+        const uint32_t v = srow[(d / DPL) * 2 * NWD + (kk & 1) * NWD + (kk >> 2)];
+        return (int)((v >> (16 * ((kk >> 1) & 1))) & 0xFFFFu);
+    };
+    const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, 16 * DPL - 1));
+    // ---- uniqueness: reject if some d outside [best-1, best+1] has S*(100-u) < minS*100.
+    // For u < 100 that is S <= thr = (minS*100 - 1) / (100 - u); with T = thr + 1 the sum of
+    // max(T - S, 0) over the row exceeds its window part exactly when such a d exists. For
+    // u >= 100 every d qualifies when minS > 0, and for u > 100, minS == 0 those with S > 0
+    // (the count of S == 0 outside the window is the same sum with T = 1).
+    int T = 0;
+    if (g.uniq < 100) {
+        if (minS > 0) {
+            const int num = minS * 100 - 1, den = 100 - g.uniq;
+            int q = (int)((float)num * inv_u);
+            q += (q + 1) * den <= num ? 1 : 0;
+            q -= q * den > num ? 1 : 0;
+            T = min(q + 1, 8 * 255 + 1);      // S <= 8 * 255: keeps the u16 sums exact
+        }
+    } else {
+        T = (minS == 0 && g.uniq > 100) ? 1 : 0;
+    }
+    const uint32_t TT = (uint32_t)T * 0x10001u;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < NWD; j++) acc += pk_subs(TT, E[j]) + pk_subs(TT, O[j]);   // halves <= 2 * NWD * 2041: no carry
+    const int tot = (int)row_sum_u32(__builtin_amdgcn_sad_u16(acc, 0u, 0u));
+    const int win = max(T - minS, 0) + (best > 0 ? max(T - sm, 0) : 0) + (best < g.D - 1 ? max(T - sp, 0) : 0);
+    int outside = tot - win;
+    if (g.uniq >= 100) {
+        const int nwin = 1 + (best > 0 ? 1 : 0) + (best < g.D - 1 ? 1 : 0);
+        outside = minS > 0 ? g.D - nwin : (g.uniq > 100 ? (g.D - nwin) - outside : 0);
+    }
+    r.rej = outside > 0;
+    const int den = max(sm + sp - 2 * minS, 1);
+    const bool use = g.subpix && best > 0 && best < g.D - 1;
+    r.d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+    r.best = best;
+    r.minS = minS;
+    return r;
+}
+
+// 0xFFFF in the S halves of a lane that hold k >= DPL or d >= D (the E / O split above)
+template <int DPL, bool EXACT>
+__device__ __forceinline__ void wta_emask(int p, const Geom& g, uint32_t (&emaskE)[(DPL + 3) / 4],
+                                          uint32_t (&emaskO)[(DPL + 3) / 4])
+{
+#pragma unroll
+    for (int j = 0; j < (DPL + 3) / 4; j++) {
+        auto bad = [&](int k) { return k >= DPL || (!EXACT && p * DPL + k >= g.D); };
+        emaskE[j] = (bad(4 * j) ? 0xFFFFu : 0u) | (bad(4 * j + 2) ? 0xFFFF0000u : 0u);
+        emaskO[j] = (bad(4 * j + 1) ? 0xFFFFu : 0u) | (bad(4 * j + 3) ? 0xFFFF0000u : 0u);
+    }
+}
+
 // One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size_t vol_bytes, const Geom& g,
@@ -646,16 +810,8 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     const size_t row0 = (size_t)y * g.width1 * g.D;
     const uint32_t off0 = (uint32_t)(lane_act ? p * DPL : 0);
     uint32_t* srow = sl + (w * 4 + r) * 32 * NWD;     // 16 lanes x 2 * NWD dwords
-    // packed-key geometry: lane-local index k in the low KB bits of a 16-bit key
-    constexpr int KB = DPL > 16 ? 5 : 4;
-    constexpr uint32_t KMASK = (1u << KB) - 1;
     uint32_t emaskE[NWD], emaskO[NWD];            // 0xFFFF in halves with k >= DPL or d >= D
-#pragma unroll
-    for (int j = 0; j < NWD; j++) {
-        auto bad = [&](int k) { return k >= DPL || (!EXACT && p * DPL + k >= g.D); };
-        emaskE[j] = (bad(4 * j) ? 0xFFFFu : 0u) | (bad(4 * j + 2) ? 0xFFFF0000u : 0u);
-        emaskO[j] = (bad(4 * j + 1) ? 0xFFFFu : 0u) | (bad(4 * j + 3) ? 0xFFFF0000u : 0u);
-    }
+    wta_emask<DPL, EXACT>(p, g, emaskE, emaskO);
     const float inv_u = 1.0f / (float)max(100 - g.uniq, 1);
     const int n = g.width1;
     const int nq = (n + 3) / 4;
@@ -668,10 +824,12 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
         const uint8_t* rowq = vols + row0 + (size_t)(4 * q) * g.D;
 #pragma unroll
-        for (int vv = 0; vv < 8; vv++) wload_buf<DPL>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
+        for (int vv = 0; vv < 8; vv++) {
+            if ((SGM_EXP & 4) && vv == 1) { for (int j = 0; j < NWD; j++) v[vv][j] = 0; continue; }
+            wload_buf<DPL>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
+        }
     };
-    // S in u16 pairs: E[j] = (S[4j], S[4j+2]), O[j] = (S[4j+1], S[4j+3]); halves past D or past
-    // the lane's DPL are 0xFFFF. The next pixel group's loads are summed at the end of an
+    // S in u16 pairs (wta_pix16). The next pixel group's loads are summed at the end of an
     // iteration, so only one set of raw volume words is live.
     uint32_t E[NWD], O[NWD];
     auto sum8 = [&](const uint32_t (&v)[8][NWD]) {
@@ -692,66 +850,14 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     sum8(nxt);
     for (int q = w; q < nq; q += 4) {
         load(min(q + 4, nq - 1), nxt);
-        // ---- (minS, best): packed 16-bit keys S << KB | k, one 16-lane min over S*512 + d ----
-        uint32_t km = 0xFFFFFFFFu;
-#pragma unroll
-        for (int j = 0; j < NWD; j++) {
-            const uint32_t ke = pk_shl(E[j], KB) | (((uint32_t)(4 * j + 2) << 16) | (uint32_t)(4 * j));
-            const uint32_t ko = pk_shl(O[j], KB) | (((uint32_t)(4 * j + 3) << 16) | (uint32_t)(4 * j + 1));
-            km = pk_min(km, pk_min(ke, ko));
-        }
-        km = pk_min(km, alignbit16(km, km)) & 0xFFFFu;      // lane min key (low half)
-        const uint32_t kmin = row_min_u32(((km >> KB) << 9) | (uint32_t)(p * DPL + (int)(km & KMASK)));
-        const int best = (int)(kmin & 511u);
-        const int minS = (int)(kmin >> 9);
-        // ---- the row's packed S slice in LDS (S[best +- 1] for subpixel and uniqueness) ----
-#pragma unroll
-        for (int j = 0; j < NWD; j++) { srow[p * 2 * NWD + j] = E[j]; srow[p * 2 * NWD + NWD + j] = O[j]; }
-        auto s_at = [&](int d) {
-            const int kk = d % DPL;
-            const uint32_t v = srow[(d / DPL) * 2 * NWD + (kk & 1) * NWD + (kk >> 2)];
-            return (int)((v >> (16 * ((kk >> 1) & 1))) & 0xFFFFu);
-        };
-        const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, 16 * DPL - 1));
-        // ---- uniqueness: reject if some d outside [best-1, best+1] has S*(100-u) < minS*100.
-        // For u < 100 that is S <= thr = (minS*100 - 1) / (100 - u); with T = thr + 1 the sum of
-        // max(T - S, 0) over the row exceeds its window part exactly when such a d exists. For
-        // u >= 100 every d qualifies when minS > 0, and for u > 100, minS == 0 those with S > 0
-        // (the count of S == 0 outside the window is the same sum with T = 1).
-        int T = 0;
-        if (g.uniq < 100) {
-            if (minS > 0) {
-                const int num = minS * 100 - 1, den = 100 - g.uniq;
-                int q = (int)((float)num * inv_u);
-                q += (q + 1) * den <= num ? 1 : 0;
-                q -= q * den > num ? 1 : 0;
-                T = min(q + 1, 8 * 255 + 1);      // S <= 8 * 255: keeps the u16 sums exact
-            }
-        } else {
-            T = (minS == 0 && g.uniq > 100) ? 1 : 0;
-        }
-        const uint32_t TT = (uint32_t)T * 0x10001u;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int j = 0; j < NWD; j++) acc += pk_subs(TT, E[j]) + pk_subs(TT, O[j]);   // halves <= 2 * NWD * 2041: no carry
-        const int tot = (int)row_sum_u32(__builtin_amdgcn_sad_u16(acc, 0u, 0u));
-        const int win = max(T - minS, 0) + (best > 0 ? max(T - sm, 0) : 0) + (best < g.D - 1 ? max(T - sp, 0) : 0);
-        int outside = tot - win;
-        if (g.uniq >= 100) {
-            const int nwin = 1 + (best > 0 ? 1 : 0) + (best < g.D - 1 ? 1 : 0);
-            outside = minS > 0 ? g.D - nwin : (g.uniq > 100 ? (g.D - nwin) - outside : 0);
-        }
-        const bool rej = outside > 0;
-        const int den = max(sm + sp - 2 * minS, 1);
-        const bool use = g.subpix && best > 0 && best < g.D - 1;
-        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const WtaPix px = wta_pix16<DPL, EXACT>(E, O, p, g, inv_u, srow);
         // ---- results: lane 0 of each row writes its pixel, the others hit dummy slots ----
         const int x1 = 4 * q + r;
         const bool wr = p == 0 && x1 < n;
         const int x = wr ? g.minX1 + x1 : g.W + lane;
-        R.bst[x] = (int16_t)(rej ? -1 : best);
-        R.mins[x] = (uint16_t)minS;
-        R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
+        R.bst[x] = (int16_t)(px.rej ? -1 : px.best);
+        R.mins[x] = (uint16_t)px.minS;
+        R.drow[(wr && !px.rej) ? x : g.W + lane] = (int16_t)px.d16;
         sum8(nxt);
     }
     R.init_key(g, tid, kWG);                      // the S slices are dead: key takes their space
@@ -848,17 +954,18 @@ __global__ __launch_bounds__(kWG) void k_census_tiles(CensusFrames cf, int W, in
     census_block(cf, W, H, blockIdx.x, tile);
 }
 
-// blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf
+// blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf.
+// wta_rows = 0: wf is served by up+WTA items (dir 8) of the work list instead of WTA rows.
 template <int DPL, bool EXACT>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : SGM_WPE)))
 void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_bytes, size_t trash_off, Geom g,
                       PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride,
-                      int period16, uint64_t* __restrict__ trace)
+                      int period16, int wta_rows, uint64_t* __restrict__ trace)
 {
     extern __shared__ uint64_t lds_dyn64[];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const int b = blockIdx.x;
-    const int n_wta = g.H * wf.n;
+    const int n_wta = wta_rows ? g.H * wf.n : 0;
     // paths and WTA blocks merged: among the first b+1 blocks, wcount(b) are WTA rows
     // (one in period16/16 blocks, period16 = 0: all WTA rows after the paths)
     auto wcount = [&](int bb) {
@@ -872,11 +979,48 @@ void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_b
         kind = is_wta ? 1 : 0;
         idx = is_wta ? w - 1 : b - w;
     }
-    if (kind == 0) paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[idx], lds_dyn64);
-    else if (kind == 1) wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, idx, (uint32_t*)lds_dyn64);
-    else census_block(cf, g.W, g.H, idx, (uint8_t*)lds_dyn64);
+    if (kind == 0) {
+        const uint32_t it = items[idx];
+        if ((it >> 24) == 8u) {             // up+WTA of frame f of wf
+            using RC = RowsCfg<DPL>;
+            const int f = (int)((it >> 22) & 3u);
+            if (f < wf.n) {
+#if SGM_UPWTA_PRIO
+                __builtin_amdgcn_s_setprio(SGM_UPWTA_PRIO);   // the launch's longest blocks
+#endif
+                const UpWta uw{pick4(wf.vols, f), vol_bytes, pick4(wf.res, f)};
+                p16_rows<RC::DPL, EXACT, RC::LPL, true>(pick4(wf.cL, f), pick4(wf.cR, f), nullptr, nullptr, g, 1,
+                                                        pl.xb_lo[1] + (int)(it & 0x3FFFFFu) * RC::NL, pl, lds_dyn64,
+                                                        uw);
+            }
+        } else {
+            paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, it, lds_dyn64);
+        }
+    } else if (kind == 1) {
+        wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, idx, (uint32_t*)lds_dyn64);
+    } else {
+        census_block(cf, g.W, g.H, idx, (uint8_t*)lds_dyn64);
+    }
     if (trace && (threadIdx.x & 63) == 0)         // debug timeline (SGM_TRACE), kind in bits 62-63
         trace_record(trace, (kind == 0 ? items[idx] : 0u) | ((uint64_t)kind << 62), t0);
+}
+
+// disp2 + LR check + store of one row from the up+WTA results: block b = row b % H of frame
+// b / H of wf (wf.res in, wf.out written)
+__global__ __launch_bounds__(kWG) void k_census_rowfin(WtaFrames wf, Geom g, size_t out_stride)
+{
+    extern __shared__ uint32_t lds_dyn[];
+    const int f = blockIdx.x / g.H, y = blockIdx.x - f * g.H;
+    const uint64_t* res = pick4(wf.res, f) + (size_t)y * g.W;
+    RowLds R(lds_dyn, g.W);
+    R.init(g, threadIdx.x, kWG, true);
+    for (int x = g.minX1 + threadIdx.x; x < g.maxX1; x += kWG) {
+        const uint64_t v = __builtin_nontemporal_load(res + x);
+        R.drow[x] = (int16_t)(uint16_t)v;
+        R.bst[x] = (int16_t)(uint16_t)(v >> 16);
+        R.mins[x] = (uint16_t)(v >> 32);
+    }
+    row_finish(g, threadIdx.x, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, pick4(wf.out, f) + (size_t)y * out_stride);
 }
 
 // ------------------------------------------------------------------------------------
@@ -916,12 +1060,21 @@ PathLaunch16 make_path_launch16(const Geom& g)
 // workgroups (consecutive workgroup ids go to different CUs, so each CU mixes long and
 // short work; with group > 1 there are more blocks than resident slots and the dispatcher
 // hands the short ones to whichever CUs drain first).
-int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, uint32_t* out, int cap)
+// up_group > 0 adds the up+WTA blocks (dir code 8, the dir-1 column blocks) of that many
+// frames of the launch's WTA group, first: they are the longest.
+int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, uint32_t* out, int cap, int up_group)
 {
     struct Item { int len; uint32_t code; };
     std::vector<Item> v;
     const PathLaunch16 pl = make_path_launch16(g);
     group = std::min(std::max(group, 1), kMaxGroup);
+    up_group = std::min(std::max(up_group, 0), kMaxGroup);
+    {
+        const int NL = rows_lines(g.D);
+        const int nb = (g.maxX1 - pl.xb_lo[1] + NL - 1) / NL;
+        for (int b = 0; b < nb; b++)
+            for (int f = 0; f < up_group; f++) v.push_back({4 * g.H + 4 * g.W, path_item(8, b, f)});
+    }
     for (int dir = 0; dir < 8; dir++) {
         if (!((dir_mask >> dir) & 1u)) continue;
         if (dir >= 6) {
@@ -978,7 +1131,11 @@ static void trace_dump(uint64_t* tr, int n_blocks, hipStream_t st)
     std::vector<uint64_t> h((size_t)n_blocks * 16);
     if (hipStreamSynchronize(st) == hipSuccess &&
         hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-        FILE* f = fopen(getenv("SGM_TRACE"), "wb");
+        // a '%d' in the name numbers the dumps (one file per traced launch)
+        static int n_dump = 0;
+        char name[512];
+        snprintf(name, sizeof name, getenv("SGM_TRACE"), n_dump++);
+        FILE* f = fopen(name, "wb");
         if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
     }
 }
@@ -1048,12 +1205,12 @@ hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& 
 template <int DPL>
 static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const CensusFrames& cf, size_t vol_bytes,
                              size_t trash_off, const Geom& g, const PathLaunch16& pl, const uint32_t* items,
-                             int n_items, size_t out_stride, hipStream_t st)
+                             int n_items, size_t out_stride, bool up_wta, hipStream_t st)
 {
     const int n_census = ((g.W + 63) / 64) * ((g.H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
-    dim3 grid(n_items + g.H * wf.n + n_census), block(kWG);
-    const size_t lds = std::max({wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * rows_lds_codes<DPL>(),
-                                 (size_t)(kCensusRows + 6) * 72});
+    dim3 grid(n_items + (up_wta ? 0 : g.H * wf.n) + n_census), block(kWG);
+    const size_t lds = std::max({up_wta ? upwta_lds_bytes<RowsCfg<DPL>::DPL>() : wta_lds_bytes<DPL>(g.W),
+                                 sizeof(uint64_t) * rows_lds_codes<DPL>(), (size_t)(kCensusRows + 6) * 72});
     uint64_t* tr = trace_buffer((int)grid.x);
     // WTA rows interleaved one per 2.5 blocks (C3 sweeps, first build: after the paths 554
     // pairs/s, 1/2 498, 1/2.5 578, 1/2.75 580, 1/3 577, 1/3.5 574; with nontemporal volumes,
@@ -1063,10 +1220,10 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
     static const int period = getenv("SGM_WTA_PERIOD") ? (int)(16 * atof(getenv("SGM_WTA_PERIOD"))) : 40;
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_fused16<DPL, true>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
-                           pl, items, n_items, out_stride, period, tr);
+                           pl, items, n_items, out_stride, period, up_wta ? 0 : 1, tr);
     else
         hipLaunchKernelGGL((k_census_fused16<DPL, false>), grid, block, lds, st, pf, wf, cf, vol_bytes, trash_off, g,
-                           pl, items, n_items, out_stride, period, tr);
+                           pl, items, n_items, out_stride, period, up_wta ? 0 : 1, tr);
     trace_dump(tr, (int)grid.x, st);
 }
 
@@ -1079,19 +1236,30 @@ hipError_t launch_census_tiles(const CensusFrames& cf, int W, int H, hipStream_t
 
 // One launch: path sweeps of the frames in pf (items), WTA of the frames in wf (the previous
 // group) and census of the frames in cf (the next group). Any of the three may be empty
-// (n_items = 0, wf.n = 0, cf.n = 0). All volume sets have the same geometry.
+// (n_items = 0, wf.n = 0, cf.n = 0). All volume sets have the same geometry. up_wta: the
+// work list carries up+WTA items for wf (its dir-1 sweeps; wf.res receives the results, and
+// launch_census_rowfin finishes the rows) instead of WTA rows.
 hipError_t launch_census_fused(const PathFrames& pf, const WtaFrames& wf, const CensusFrames& cf, size_t vol_bytes,
-                               const Geom& g, const uint32_t* items, int n_items, size_t out_stride, hipStream_t st)
+                               const Geom& g, const uint32_t* items, int n_items, size_t out_stride, bool up_wta,
+                               hipStream_t st)
 {
     const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
-    case 2: launch_fused_dpl<2>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 4: launch_fused_dpl<4>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 8: launch_fused_dpl<8>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    case 16: launch_fused_dpl<16>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
-    default: launch_fused_dpl<32>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, st); break;
+    case 2: launch_fused_dpl<2>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;
+    case 4: launch_fused_dpl<4>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;
+    case 8: launch_fused_dpl<8>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;
+    case 16: launch_fused_dpl<16>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;
+    default: launch_fused_dpl<32>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;
     }
+    return hipGetLastError();
+}
+
+// disp2 + LR + store of every row of the frames in wf from their up+WTA results
+hipError_t launch_census_rowfin(const WtaFrames& wf, const Geom& g, size_t out_stride, hipStream_t st)
+{
+    if (wf.n > 0)
+        hipLaunchKernelGGL(k_census_rowfin, dim3(g.H * wf.n), dim3(kWG), RowLds::bytes(g.W), st, wf, g, out_stride);
     return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@
 
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
-int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int);
+int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int, int up_group = 0);
 hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t,
                                const uint8_t* = nullptr, const uint8_t* = nullptr, size_t = 0);
 hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
@@ -36,8 +36,8 @@ void cubic_table(int16_t*);
 bool rectify_inverse(const double*, const double*, double*);
 hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
-                               const uint32_t*, int, size_t,
-                               hipStream_t);
+                               const uint32_t*, int, size_t, bool, hipStream_t);
+hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -282,16 +282,28 @@ int ensure_cubic_table(sgm_handle* h)
 
 // Workspace carve-up for one geometry. Offsets are 256-B aligned.
 struct Layout {
-    // census: set 0 serves single matches; a pipelined batch uses sets 0 .. 2*group-1
-    size_t cL[2 * sgm::kMaxGroup] = {}, cR[2 * sgm::kMaxGroup] = {}, vols[2 * sgm::kMaxGroup] = {};
+    // census: set 0 serves single matches; a pipelined batch uses code sets 0 .. 3*group-1
+    // (the census of group k+1 runs beside the up+WTA sweeps of group k-1), volume sets
+    // 0 .. 2*group-1 and one up+WTA result image per frame of a group
+    size_t cL[3 * sgm::kMaxGroup] = {}, cR[3 * sgm::kMaxGroup] = {}, vols[2 * sgm::kMaxGroup] = {};
+    size_t res[sgm::kMaxGroup] = {};
     size_t vol_bytes = 0;
     int group = 1;                                         // frames per pipelined launch
+    bool up_wta = false;                                   // pipelined batch: up+WTA scheme
     size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0;                      // host-API staging
     size_t total = 0;
 };
+
+// Pipelined census batches fuse the upward vertical sweep with the WTA (census_sgm.hip
+// UpWta) unless SGM_UPWTA=0 (the earlier scheme: 8 volumes written, WTA rows interleaved).
+bool use_up_wta()
+{
+    const char* e = std::getenv("SGM_UPWTA");
+    return !e || std::atoi(e) != 0;
+}
 
 Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group = 0)
 {
@@ -304,17 +316,20 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     if (p.mode == SGM_MODE_CENSUS8) {
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
         l.group = std::max(group, 1);
+        l.up_wta = group > 0 && use_up_wta();
         const int sets = group > 0 ? 2 * l.group : 1;
-        for (int i = 0; i < sets; i++) {
+        for (int i = 0; i < sets; i++) l.vols[i] = take(l.vol_bytes * 8);
+        for (int i = 0; i < (l.up_wta ? 3 * l.group : sets); i++) {
             l.cL[i] = take_codes(WH);
             l.cR[i] = take_codes(WH);
-            l.vols[i] = take(l.vol_bytes * 8);
         }
+        if (l.up_wta)
+            for (int i = 0; i < l.group; i++) l.res[i] = take((WH + 64) * 8);
         if (g.width1 > 0) {
             l.n_items[0] = sgm::census_path_items(g, 0xFFu, 1, 1, nullptr, 0);
             l.items[0] = take((size_t)l.n_items[0] * 4);
             if (group > 0) {
-                l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0);
+                l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0, l.up_wta ? l.group : 0);
                 l.items[1] = take((size_t)l.n_items[1] * 4);
             }
         }
@@ -364,14 +379,15 @@ struct StageRec {
 // Device work list of the census path launch for (g, only_dir), uploaded on `st` when the
 // geometry or the workspace changed. Returns the entry count (< 0: error).
 int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask, int group, hipStream_t st,
-               const uint32_t** dev)
+               const uint32_t** dev, int up_group = 0)
 {
-    const int w = group > 1 ? 1 : 0;
+    const int w = group > 1 || up_group > 0 ? 1 : 0;
     uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items[w]);
     *dev = d;
     char key[160];
-    snprintf(key, sizeof key, "%d %d %d %d %x %d %d %p", g.W, g.H, g.D, g.minD, dir_mask, group, h->n_cu, (void*)d);
-    const int n = sgm::census_path_items(g, dir_mask, h->n_cu, group, nullptr, 0);
+    snprintf(key, sizeof key, "%d %d %d %d %x %d %d %d %p", g.W, g.H, g.D, g.minD, dir_mask, group, up_group, h->n_cu,
+             (void*)d);
+    const int n = sgm::census_path_items(g, dir_mask, h->n_cu, group, nullptr, 0, up_group);
     if (h->items_key[w] == key) return n;
     if (n > l.n_items[w]) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
     if (n > h->items_cap) {
@@ -381,7 +397,7 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask,
         HIP_TRY(hipHostMalloc((void**)&h->items_pin, (size_t)n * 4, hipHostMallocDefault), "hipHostMalloc");
         h->items_cap = n;
     }
-    sgm::census_path_items(g, dir_mask, h->n_cu, group, h->items_pin, h->items_cap);
+    sgm::census_path_items(g, dir_mask, h->n_cu, group, h->items_pin, h->items_cap, up_group);
     HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
     HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
     h->items_key[w] = key;
@@ -498,13 +514,21 @@ int batch_group(int n)
     return std::max(1, std::min({g, sgm::kMaxGroup, n}));
 }
 
-// Census-mode frame pipeline on h->stream, in groups of l.group frames (sets 2*group):
+// Census-mode frame pipeline on h->stream, in groups of l.group frames.
+// up+WTA scheme (l.up_wta, the default):
+//   census(G0) | fused[paths7(G0) + census(G1)] | fused[paths7(Gk) + upWTA(Gk-1) + census(Gk+1)]
+//   rowfin(Gk-1) post(Gk-1) ... | fused[paths8(Glast) + upWTA(Glast-1)] rowfin post | wta(Glast) post
+// paths7 = the seven directions other than dir 1 (volumes written); upWTA = the dir-1 sweep
+// of the previous group with its WTA fused (census_sgm.hip UpWta: volume 1 is never stored),
+// rowfin = disp2 + LR of those rows. Codes rotate over three sets (group k+1's census runs
+// beside group k-1's dir-1 sweep), volumes over two.
+// Earlier scheme (SGM_UPWTA=0):
 //   census(G0) | fused[paths(G0) + census(G1)] | fused[paths(Gk) + wta(Gk-1) + census(Gk+1)] post(Gk-1)
 //   ... | wta(Glast) post
 // The census of group k+1 writes the code set of group k-1, whose path sweeps finished in
-// the previous launch. With a median the WTA of a group writes each frame's raw disparity
-// to its own scratch image (post filters read it), so no frame's output is overwritten
-// before its median.
+// the previous launch.
+// With a median the WTA of a group writes each frame's raw disparity to its own scratch image
+// (post filters read it), so no frame's output is overwritten before its median.
 // With h->rect_on, dLs / dRs are raw images (stride = raw stride) rectified inside the census
 // (the census tiles read remap(raw)), and rectLs / rectRs (may be null) receive the
 // rectified images.
@@ -520,21 +544,22 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
     const double WH = (double)g.W * g.H;
     const double cells = (double)g.width1 * g.H * g.D;
     const int G = l.group;
+    const bool up = l.up_wta;
     const int ng = (n + G - 1) / G;
     const uint32_t* items;
-    const int n_items = path_items(h, l, g, 0xFFu, G, st, &items);
+    const int n_items = path_items(h, l, g, 0xFFu, G, st, &items, up ? G : 0);
     if (n_items < 0) return n_items;
     StageRec rec{h};
     if (h->profiling) h->prof_frames += n;
     auto frames_of = [&](int k) { return std::min(G, n - k * G); };
+    auto code_set = [&](int k, int f) { return (up ? k % 3 : k & 1) * G + f; };
     auto path_frames = [&](int k) {
         sgm::PathFrames pf{};
         pf.n = frames_of(k);
         for (int f = 0; f < pf.n; f++) {
-            const int set = (k & 1) * G + f;
-            pf.cL[f] = (const uint64_t*)(ws + l.cL[set]);
-            pf.cR[f] = (const uint64_t*)(ws + l.cR[set]);
-            pf.vols[f] = (uint8_t*)(ws + l.vols[set]);
+            pf.cL[f] = (const uint64_t*)(ws + l.cL[code_set(k, f)]);
+            pf.cR[f] = (const uint64_t*)(ws + l.cR[code_set(k, f)]);
+            pf.vols[f] = (uint8_t*)(ws + l.vols[(k & 1) * G + f]);
         }
         return pf;
     };
@@ -545,6 +570,11 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         for (int f = 0; f < wf.n; f++) {
             wf.vols[f] = (const uint8_t*)(ws + l.vols[(k & 1) * G + f]);
             wf.out[f] = med ? (int16_t*)(ws + l.tmp) + (size_t)f * g.W * g.H : outs[k * G + f];
+            if (up) {
+                wf.cL[f] = (const uint64_t*)(ws + l.cL[code_set(k, f)]);
+                wf.cR[f] = (const uint64_t*)(ws + l.cR[code_set(k, f)]);
+                wf.res[f] = (uint64_t*)(ws + l.res[f]);
+            }
         }
         return wf;
     };
@@ -555,11 +585,10 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         cf.rect_stride = rect_stride;
         if (h->rect_on) cf.rect = h->rect;
         for (int f = 0; f < cf.n; f++) {
-            const int set = (k & 1) * G + f;
             cf.L[f] = dLs[k * G + f];
             cf.R[f] = dRs[k * G + f];
-            cf.cL[f] = (uint64_t*)(ws + l.cL[set]);
-            cf.cR[f] = (uint64_t*)(ws + l.cR[set]);
+            cf.cL[f] = (uint64_t*)(ws + l.cL[code_set(k, f)]);
+            cf.cR[f] = (uint64_t*)(ws + l.cR[code_set(k, f)]);
             cf.rectL[f] = rectLs ? rectLs[k * G + f] : nullptr;
             cf.rectR[f] = rectRs ? rectRs[k * G + f] : nullptr;
         }
@@ -577,16 +606,36 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
     } else {
         for (int f = 0; f < frames_of(0); f++) {
             rec.begin("census", 2 * WH + 16 * WH);
-            HIP_TRY(sgm::launch_census(dLs[f], dRs[f], stride, g.W, g.H, (uint64_t*)(ws + l.cL[f]),
-                                       (uint64_t*)(ws + l.cR[f]), st), "census");
+            HIP_TRY(sgm::launch_census(dLs[f], dRs[f], stride, g.W, g.H, (uint64_t*)(ws + l.cL[code_set(0, f)]),
+                                       (uint64_t*)(ws + l.cR[code_set(0, f)]), st), "census");
         }
     }
     for (int k = 0; k <= ng; k++) {
         // this launch reads the inputs of group k + 1 (census in the tail) and writes the
-        // disparities of group k - 1 (WTA)
+        // disparities of group k - 1 (WTA, or up+WTA and the row finish after it)
         if (k + 1 < ng && ng > 1 && (hrc = hk_in(k + 1))) return hrc;
         if (k > 0 && (hrc = hk_free(k - 1))) return hrc;
-        if (k == ng) {
+        if (up && k < ng) {
+            // the last group sweeps all eight directions (its WTA rows follow alone: a lone
+            // launch of up+WTA blocks would be one long latency-bound chain per column block)
+            const bool last = k == ng - 1;
+            sgm::PathFrames pf = path_frames(k);
+            pf.skip_dirs = last ? 0u : 2u;
+            const sgm::WtaFrames wf = k > 0 ? wta_frames(k - 1) : sgm::WtaFrames{};
+            const sgm::CensusFrames cf = k + 1 < ng ? census_frames(k + 1) : sgm::CensusFrames{};
+            // stage name and algorithmic bytes (the canonical dataflow: the dir-1 volume of an
+            // up+WTA frame counted as written and read, as if it existed) from the launch's parts
+            const char* name = last ? (wf.n ? "paths8+up_wta" : "paths8")
+                                    : (wf.n ? (cf.n ? "paths7+up_wta+census" : "paths7+up_wta")
+                                            : (cf.n ? "paths7+census" : "paths7"));
+            rec.begin(name, (last ? 8 : 7) * cells * pf.n + (9 * cells + 2 * WH) * wf.n + 18 * WH * cf.n);
+            HIP_TRY(sgm::launch_census_fused(pf, wf, cf, l.vol_bytes, g, items, n_items, dst_stride, true, st),
+                    "fused");
+            if (wf.n) {
+                rec.begin("rowfin", 10 * WH * wf.n);
+                HIP_TRY(sgm::launch_census_rowfin(wf, g, dst_stride, st), "rowfin");
+            }
+        } else if (k == ng) {
             rec.begin("wta_lr", (8 * cells + 2 * WH) * frames_of(k - 1));
             HIP_TRY(sgm::launch_census_wta(wta_frames(k - 1), l.vol_bytes, g, dst_stride, st), "wta");
         } else if (ng == 1) {
@@ -595,10 +644,10 @@ int run_batch_census(sgm_handle* h, const Layout& l, const Geom& g, const uint8_
         } else {
             const sgm::WtaFrames wf = k > 0 ? wta_frames(k - 1) : sgm::WtaFrames{};
             const sgm::CensusFrames cf = k + 1 < ng ? census_frames(k + 1) : sgm::CensusFrames{};
-            // stage name and algorithmic bytes from the parts this launch carries
             const char* name = wf.n ? (cf.n ? "paths8+wta_lr+census" : "paths8+wta_lr") : "paths8+census";
             rec.begin(name, 8 * cells * frames_of(k) + (8 * cells + 2 * WH) * wf.n + 18 * WH * cf.n);
-            HIP_TRY(sgm::launch_census_fused(path_frames(k), wf, cf, l.vol_bytes, g, items, n_items, dst_stride, st),
+            HIP_TRY(sgm::launch_census_fused(path_frames(k), wf, cf, l.vol_bytes, g, items, n_items, dst_stride, false,
+                                             st),
                     "fused");
         }
         if (k > 0) {

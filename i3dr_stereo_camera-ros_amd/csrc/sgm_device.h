@@ -245,11 +245,16 @@ struct PathFrames {
     const uint64_t* cR[kMaxGroup];
     uint8_t* vols[kMaxGroup];
     int n;
+    unsigned skip_dirs;     // work-list directions this launch skips (bit d: direction d)
 };
 struct WtaFrames {
     const uint8_t* vols[kMaxGroup];
     int16_t* out[kMaxGroup];
     int n;
+    // up+WTA blocks (census_sgm.hip UpWta): the frames' codes and per-pixel result images
+    const uint64_t* cL[kMaxGroup];
+    const uint64_t* cR[kMaxGroup];
+    uint64_t* res[kMaxGroup];
 };
 // Rectification fused into the census: the census tile reads
 // remap(raw, map) instead of a rectified image. map[0..1] = left x/y, map[2..3] = right x/y,

@@ -187,14 +187,18 @@ def test_profiling_stage_times(engine, pkg, synth):
     assert all(t >= 0 for _, t, _ in st) and all(b > 0 for _, _, b in st)
 
 
+@pytest.mark.parametrize("up_wta", [1, 0])
 @pytest.mark.parametrize("kw,n", [(dict(num_disparities=64), 2), (dict(num_disparities=48, min_disparity=3), 3),
                                   (dict(num_disparities=128, median=1, speckle_window_size=20, speckle_range=2), 4),
                                   (dict(num_disparities=256), 5), (dict(num_disparities=32), 1),
                                   (dict(num_disparities=400, median=1), 7)])
-def test_device_batch_pipeline(engine, oracle, pkg, synth, kw, n):
-    """sgm_match_device_batch (paths of frame i+1 fused with the WTA of frame i) returns
-    exactly the per-frame results, for every frame of the batch."""
+def test_device_batch_pipeline(engine, oracle, pkg, synth, monkeypatch, kw, n, up_wta):
+    """sgm_match_device_batch (the sweeps of one group of frames fused with the WTA of the
+    previous group) returns exactly the per-frame results, for every frame of the batch, in
+    both schemes: the up+WTA one (the previous group's upward sweep carries its WTA, so its
+    volume is never stored) and the earlier one (SGM_UPWTA=0: eight volumes, WTA rows)."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("SGM_UPWTA", str(up_wta))
     D, minD = kw["num_disparities"], kw.get("min_disparity", 0)
     h, w = 45, max(D + minD, 0) + 150
     p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
@@ -216,15 +220,28 @@ def test_device_batch_pipeline(engine, oracle, pkg, synth, kw, n):
     for i, (l, r, _) in enumerate(frames):
         ref = oracle.match(op, l, r)
         assert np.array_equal(got[i], ref), f"frame {i}: {(got[i] != ref).sum()} pixels differ"
-    # groups of (default) 2 frames: census(G0) | fused[paths(G0) + census(G1)] |
-    # fused[paths(Gk) + wta(Gk-1) + census(Gk+1)] ... | fused[paths(Glast) + wta] | wta(Glast)
-    ng = (n + 1) // 2
-    assert launches["census"] == min(n, 2) and launches["wta_lr"] == 1
-    if ng == 1:
-        assert launches["paths8"] == 1
+    ng = (n + 1) // 2         # groups of (default) 2 frames
+    assert launches["census"] == min(n, 2)
+    if n == 1:                # one frame: the single-frame pipeline (no group to fuse with)
+        assert launches["paths8"] == 1 and launches["wta_lr"] == 1
+    elif up_wta:
+        # census(G0) | fused[paths7(G0) + census(G1)] | fused[paths7(Gk) + upWTA(Gk-1) + census(Gk+1)]
+        # rowfin ... | fused[paths8(Glast) + upWTA(Glast-1)] rowfin | wta(Glast)
+        assert launches["wta_lr"] == 1 and launches.get("rowfin", 0) == ng - 1
+        if ng == 1:
+            assert launches["paths8"] == 1
+        else:
+            assert launches["paths7+census"] == 1 and launches["paths8+up_wta"] == 1
+            assert launches.get("paths7+up_wta+census", 0) == ng - 2
     else:
-        assert launches["paths8+census"] == 1 and launches["paths8+wta_lr"] == 1
-        assert launches.get("paths8+wta_lr+census", 0) == ng - 2
+        # census(G0) | fused[paths(G0) + census(G1)] | fused[paths(Gk) + wta(Gk-1) + census(Gk+1)]
+        # ... | fused[paths(Glast) + wta] | wta(Glast)
+        assert launches["wta_lr"] == 1
+        if ng == 1:
+            assert launches["paths8"] == 1
+        else:
+            assert launches["paths8+census"] == 1 and launches["paths8+wta_lr"] == 1
+            assert launches.get("paths8+wta_lr+census", 0) == ng - 2
 
 
 def test_tiled_single_band_is_exact(engine, oracle, synth, pkg):
