@@ -57,9 +57,10 @@ def algorithmic_bytes(w, h, D, width1=None):
     return 4.0 * w * h + 16.0 * (w if width1 is None else width1) * h * D
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch from the committed PMC profile (profiles/*_pmc.json), if any."""
-    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+def load_pmc_traffic(config):
+    """HBM bytes per launch from the committed PMC profile (profiles/latest_pmc_<config>.json,
+    written by tools/refresh_profiles.sh with the source revision it profiled), if any."""
+    path = os.path.join(ROOT, "profiles", f"latest_pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
@@ -275,11 +276,11 @@ def main():
             pipe_achieved_w1 = b_alg_w1 / (dev_frame_ms * 1e-3) / 1e9
             # HBM bytes from PMC counters need rocprofv3 (a separate run): `traffic` stays null
             # here; the committed PMC summary of the same launch kind is quoted beside it
-            pmc = load_pmc_traffic()
+            pmc = load_pmc_traffic(args.config)
             traffic_profile = None
             if pmc and pmc.get("config") == args.config and dom[0] in pmc.get("kernels", {}):
                 traffic_profile = {"hbm_bytes_per_launch": pmc["kernels"][dom[0]].get("hbm_bytes_per_launch"),
-                                   "source": "profiles/latest_pmc.json (rocprofv3 --pmc, separate run; "
+                                   "source": f"profiles/latest_pmc_{args.config}.json (rocprofv3 --pmc, separate run; "
                                              "tools/refresh_profiles.sh)", "git": pmc.get("git")}
             roofline = {"bound": "hbm", "kernel": dom[0], "achieved": round(dom_achieved, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom_achieved / HBM_PEAK_GBS, 4),

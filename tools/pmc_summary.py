@@ -22,6 +22,9 @@ def main():
     ap.add_argument("dir", nargs="?", default="gpurun_out/pmc")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--steady-name", default="paths7+up_wta+census",
+                    help="bench stage name of the largest-grid fused launch (SGM_UPWTA=0: paths8+wta_lr+census)")
+    ap.add_argument("--git", default=None, help="source revision the profiled build came from")
     args = ap.parse_args()
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     grids = collections.defaultdict(set)
@@ -41,7 +44,7 @@ def main():
             # the steady-state launch (paths of group k + WTA of k-1 + census of k+1) has the
             # largest grid; the pipeline's ramp launches are reported by grid size
             g = int(k.split("@grid")[1])
-            stage = "paths8+wta_lr+census" if g == max(grids[k.split("@")[0]]) else f"fused@grid{g}"
+            stage = args.steady_name if g == max(grids[k.split("@")[0]]) else f"fused@grid{g}"
         if stage is None or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
         fetch = 2.0 * cs["FETCH_SIZE"] * 1024.0
@@ -50,7 +53,13 @@ def main():
                           "hbm_bytes_per_launch": fetch + write,
                           "valu_insts": cs.get("SQ_INSTS_VALU"), "salu_insts": cs.get("SQ_INSTS_SALU"),
                           "lds_insts": cs.get("SQ_INSTS_LDS")}
-    out = {"config": args.config, "source": "rocprofv3 --pmc (tools/pmc.sh), mean per dispatch",
+        if cs.get("SQ_INSTS_VALU") and cs.get("GRBM_GUI_ACTIVE"):
+            # launch cycles = GRBM_GUI_ACTIVE / 8 XCDs; VALU issue ~4.2 cycles per wave64
+            # instruction per SIMD for the path engine's mix, 1024 SIMDs
+            cyc = cs["GRBM_GUI_ACTIVE"] / 8.0
+            kernels[stage]["launch_cycles"] = cyc
+            kernels[stage]["valu_busy_est"] = cs["SQ_INSTS_VALU"] / 1024.0 * 4.2 / cyc
+    out = {"config": args.config, "git": args.git, "source": "rocprofv3 --pmc (tools/pmc.sh), mean per dispatch",
            "kernels": kernels, "raw": raw}
     s = json.dumps(out, indent=1)
     if args.out:
