@@ -25,6 +25,10 @@ constexpr int kMaxCost = 32767;
 #ifndef SGM_OCV_PF
 #define SGM_OCV_PF 8       // cost rows in flight per path line (D <= 64)
 #endif
+#ifndef SGM_OCV_PF_WIDE
+#define SGM_OCV_PF_WIDE 2  // the same for more disparities per lane (1080p D=128 MODE_SGBM paths:
+                           // 1 step 1.42 ms, 2 steps 0.95, 3 steps 1.57, 4 steps 1.25)
+#endif
 
 __global__ __launch_bounds__(256) void k_ocv_prefilter(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                        size_t stride, int W, int H, int ftzero,
@@ -97,26 +101,39 @@ __global__ __launch_bounds__(256) void k_ocv_hsum(const int16_t* __restrict__ pi
     }
 }
 
-// Pixel cost + horizontal SAD box fused: one block per XB output pixels of a row. The BT
-// intervals of both images and the pixel costs of the XB + 2*SW2 columns the box reads
-// (positions clamped to [0, width1), as the running sum's replicate rule) live in LDS; the
-// box is a direct (2*SW2+1)-term sum of them — the same integer as the running sum.
-constexpr int kPixXB = 32;
+// Pixel cost + horizontal SAD box fused: one block per XB output pixels x DC disparities of
+// a row (blockIdx.z: the disparity chunk). The BT intervals of both images and the pixel
+// costs of the XB + 2*SW2 columns the box reads (positions clamped to [0, width1), as the
+// running sum's replicate rule) live in LDS; the box is a direct (2*SW2+1)-term sum of them —
+// the same integer as the running sum. Chunking the disparities lets a block take many
+// output columns (few halo columns recomputed) at any D: the shipped 2448x2048 D=480 block-21
+// config went 5.38 -> see DESIGN (XB 32 x all 480 d: 52 staged columns per 32 outputs, 51 KB).
+constexpr int kPixXB = 128;     // output columns per block
+constexpr int kPixDC = 128;     // disparities per block
+__host__ __device__ inline int pix_xb(const Geom& g) { return g.D >= kPixDC ? kPixXB : kPixXB * 2; }
+__host__ __device__ inline int pix_dc(const Geom& g) { return g.D < kPixDC ? g.D : kPixDC; }
+__host__ inline size_t pix_lds_bytes(const Geom& g)
+{
+    const int XB = pix_xb(g), DC = pix_dc(g), NX = XB + 2 * g.SW2;
+    return (((size_t)2 * NX * DC + 7) & ~(size_t)7) + 8 * NX + 8 * (NX + DC - 1);
+}
 __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__ planes, Geom g,
                                                      int16_t* __restrict__ hs)
 {
     extern __shared__ uint8_t lds_pix[];
-    const int y = blockIdx.y, x0 = blockIdx.x * kPixXB, tid = threadIdx.x;
-    const int SW2 = g.SW2, NX = kPixXB + 2 * SW2;          // pixel-cost columns staged
-    const int NR = NX + g.D - 1;                           // right-image BT entries needed
+    const int XB = pix_xb(g), DCmax = pix_dc(g);
+    const int y = blockIdx.y, x0 = blockIdx.x * XB, tid = threadIdx.x;
+    const int d0 = blockIdx.z * DCmax, DC = min(DCmax, g.D - d0);
+    const int SW2 = g.SW2, NX = XB + 2 * SW2;              // pixel-cost columns staged
+    const int NR = NX + DC - 1;                            // right-image BT entries needed
     const size_t plane = (size_t)g.W * g.H;
-    int16_t* P = (int16_t*)lds_pix;                        // [NX][D]
+    int16_t* P = (int16_t*)lds_pix;                        // [NX][DC]
     // BT intervals as 8-byte records (u, lo, hi of channel 0, then of channel 1, 2 pad):
     // a cell's six reads per side share one address (immediate offsets), which matters
     // because this kernel is VALU-bound (one address add per read otherwise)
-    uint8_t* bl = lds_pix + (((size_t)2 * NX * g.D + 7) & ~(size_t)7);   // left  [NX] records
-    uint8_t* br = bl + 8 * NX;                                           // right [NR] records
-    // staged column i -> x1 = clamp(x0 - SW2 + i); right entry r -> xr = xlo - minD - (D-1) + r
+    uint8_t* bl = lds_pix + (((size_t)2 * NX * DC + 7) & ~(size_t)7);   // left  [NX] records
+    uint8_t* br = bl + 8 * NX;                                          // right [NR] records
+    // staged column i -> x1 = clamp(x0 - SW2 + i); right entry r -> xr = xlo - minD - (d0+DC-1) + r
     const int xlo = g.minX1 + min(max(x0 - SW2, 0), g.width1 - 1);
     for (int i = tid; i < 2 * NX; i += 256) {
         const int c = i / NX, k = i - c * NX;
@@ -125,7 +142,7 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         bt_lohi(planes + c * plane + (size_t)y * g.W, x, g.W, u, lo, hi);
         bl[8 * k + 3 * c] = (uint8_t)u; bl[8 * k + 3 * c + 1] = (uint8_t)lo; bl[8 * k + 3 * c + 2] = (uint8_t)hi;
     }
-    const int xr0 = xlo - g.minD - (g.D - 1);
+    const int xr0 = xlo - g.minD - (d0 + DC - 1);
     for (int i = tid; i < 2 * NR; i += 256) {
         const int c = i / NR, r = i - c * NR;
         const int xr = min(max(xr0 + r, 0), g.W - 1);
@@ -134,13 +151,13 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         br[8 * r + 3 * c] = (uint8_t)v; br[8 * r + 3 * c + 1] = (uint8_t)lo; br[8 * r + 3 * c + 2] = (uint8_t)hi;
     }
     __syncthreads();
-    // (k, d) of flat index i = k * D + d, advanced by 256 per iteration without divisions
-    const int kstep = 256 / g.D, dstep = 256 - kstep * g.D;
-    int k = tid / g.D, d = tid - k * g.D;
-    for (int i = tid; i < NX * g.D; i += 256) {
+    // (k, d) of flat index i = k * DC + d, advanced by 256 per iteration without divisions
+    const int kstep = 256 / DC, dstep = 256 - kstep * DC;
+    int k = tid / DC, d = tid - k * DC;
+    for (int i = tid; i < NX * DC; i += 256) {
         const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
         const uint8_t* L8 = bl + 8 * k;
-        const uint8_t* R8 = br + 8 * (x - g.minD - d - xr0);   // entry of xr = x - minD - d
+        const uint8_t* R8 = br + 8 * (x - g.minD - (d0 + d) - xr0);   // entry of xr = x - minD - d
         int acc = 0;
 #pragma unroll
         for (int c = 0; c < 2; c++) {
@@ -152,25 +169,25 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
         }
         P[i] = (int16_t)acc;
         k += kstep; d += dstep;
-        if (d >= g.D) { d -= g.D; k++; }
+        if (d >= DC) { d -= DC; k++; }
     }
     __syncthreads();
     // horizontal box: thread (segment, d) slides its window over the segment's outputs
     // (2 LDS reads per output after the first; int sums, so any order is exact)
-    const int nout = min(kPixXB, g.width1 - x0);
-    int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D;     // the block's outputs are contiguous
-    const int nseg = max(256 / g.D, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
-    for (int t = tid; t < nseg * g.D; t += 256) {
-        const int seg = t / g.D, dd = t - seg * g.D;
+    const int nout = min(XB, g.width1 - x0);
+    int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D + d0;
+    const int nseg = max(256 / DC, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
+    for (int t = tid; t < nseg * DC; t += 256) {
+        const int seg = t / DC, dd = t - seg * DC;
         const int xa = seg * seglen, xb = min(xa + seglen, nout);
         if (xa >= xb) continue;
         const int16_t* Pd = P + dd;
         int sum = 0;
-        for (int u = 0; u <= BW; u++) sum += Pd[(xa + u) * g.D];
-        dst[xa * g.D + dd] = (int16_t)sum;
+        for (int u = 0; u <= BW; u++) sum += Pd[(xa + u) * DC];
+        dst[(size_t)xa * g.D + dd] = (int16_t)sum;
         for (int xo = xa + 1; xo < xb; xo++) {
-            sum += Pd[(xo + BW) * g.D] - Pd[(xo - 1) * g.D];
-            dst[xo * g.D + dd] = (int16_t)sum;
+            sum += Pd[(xo + BW) * DC] - Pd[(xo - 1) * DC];
+            dst[(size_t)xo * g.D + dd] = (int16_t)sum;
         }
     }
 }
@@ -497,7 +514,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // one vector load per lane (lanes past D read the last valid group: their C never
     // reaches an entry with d < D): no exec-masked branch around the loads, so the prefetch
     // keeps counted waits
-    constexpr int PF = DPL <= 4 ? SGM_OCV_PF : 4;
+    constexpr int PF = DPL <= 4 ? SGM_OCV_PF : SGM_OCV_PF_WIDE;
     int Cb[PF][DPL];
     const bool lane_act = p * DPL < g.D;
     const int dl = min(p * DPL, g.D - DPL);
@@ -660,11 +677,11 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 {
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes);
-    const int NX = kPixXB + 2 * g.SW2;
-    const size_t lds = (((size_t)2 * NX * g.D + 7) & ~(size_t)7) + 8 * NX + 8 * (NX + g.D - 1);
+    const size_t lds = pix_lds_bytes(g);
     if (lds <= 64 * 1024) {
-        hipLaunchKernelGGL(k_ocv_pixhsum, dim3((g.width1 + kPixXB - 1) / kPixXB, g.H), dim3(256), lds, st, planes, g,
-                           bufB);
+        const int XB = pix_xb(g), DC = pix_dc(g);
+        hipLaunchKernelGGL(k_ocv_pixhsum, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256), lds, st,
+                           planes, g, bufB);
     } else {                // very wide boxes x wide ranges: the unfused pair (no LDS staging)
         hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
         hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
@@ -717,7 +734,9 @@ constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lane
 static int ocv_lanes_per_line(const Geom& g, int dirmask)
 {
     if (g.D <= 32) return 16;
-    if (g.D > 256 && g.D % 32 != 0) return 32;       // 16 lanes x DPL 32 would straddle D
+    if (g.D > 256) return 32;       // 16 lanes x DPL 32 would straddle D when D % 32 = 16, and
+                                    // its 32-value step is slower anyway (the shipped 2448x2048
+                                    // D=480 config, MODE_SGBM paths: 17.4 ms vs 8.8 ms)
     if (const char* e = getenv("SGM_OCV_LPL")) return atoi(e) == 32 ? 32 : 16;
     int waves = 0;
     for (int i = 0; i < 8; i++)
@@ -741,8 +760,7 @@ hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t cells, const Ge
         case 2: launch_ocv_paths_v<2, 16>(C, vols, cells, g, dirmask, st); break;
         case 4: launch_ocv_paths_v<4, 16>(C, vols, cells, g, dirmask, st); break;
         case 8: launch_ocv_paths_v<8, 16>(C, vols, cells, g, dirmask, st); break;
-        case 16: launch_ocv_paths_v<16, 16>(C, vols, cells, g, dirmask, st); break;
-        default: launch_ocv_paths_v<32, 16>(C, vols, cells, g, dirmask, st); break;
+        default: launch_ocv_paths_v<16, 16>(C, vols, cells, g, dirmask, st); break;   // D <= 256 here
         }
     }
     return hipGetLastError();

@@ -67,7 +67,8 @@ def test_ocv_node_defaults_c1(engine, oracle, synth, pkg, mode):
 @pytest.mark.parametrize("nobuf", ["", "1"], ids=["buf32", "ptr64"])
 @pytest.mark.parametrize("lanes", ["16", "32"])
 @pytest.mark.parametrize("mode,h,w,minD,D,block", [(0, 480, 640, 9, 64, 15), (1, 96, 500, 0, 128, 5),
-                                                   (0, 40, 600, -4, 256, 7), (1, 33, 200, 3, 48, 3)])
+                                                   (0, 40, 600, -4, 256, 7), (1, 33, 200, 3, 48, 3),
+                                                   (1, 24, 640, -3, 480, 9), (0, 20, 700, 147, 400, 21)])
 def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf, lanes, mode, h, w, minD, D, block):
     """Both path-kernel shapes (16 and 32 lanes per line, SGM_OCV_LPL) and both addressing
     schemes (32-bit buffer offsets; the 64-bit clamped pointers of > 2 GB volumes,
