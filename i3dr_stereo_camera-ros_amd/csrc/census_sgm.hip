@@ -14,6 +14,9 @@
 #ifndef SGM_WPE
 #define SGM_WPE 4          // minimum waves per SIMD of the path kernels (register budget)
 #endif
+#ifndef SGM_WPE32
+#define SGM_WPE32 4        // the same for 32 disparities per lane (D > 256; 2: C5 single frame 27.4 vs 23.9 ms)
+#endif
 #ifndef SGM_NT_STORE
 #define SGM_NT_STORE 1     // path volumes written with nontemporal stores (0: plain)
 #endif
@@ -675,7 +678,7 @@ __device__ __forceinline__ void trace_record(uint64_t* trace, uint64_t tag, uint
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : SGM_WPE)))
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? SGM_WPE32 : SGM_WPE)))
 void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
                       const uint32_t* __restrict__ items, uint64_t* __restrict__ trace)
 {
@@ -957,7 +960,7 @@ __global__ __launch_bounds__(kWG) void k_census_tiles(CensusFrames cf, int W, in
 // blocks: [0, n_items) path items of pf | H * wf.n WTA rows of wf | census blocks of cf.
 // wta_rows = 0: wf is served by up+WTA items (dir 8) of the work list instead of WTA rows.
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? 2 : SGM_WPE)))
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? SGM_WPE32 : SGM_WPE)))
 void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_bytes, size_t trash_off, Geom g,
                       PathLaunch16 pl, const uint32_t* __restrict__ items, int n_items, size_t out_stride,
                       int period16, int wta_rows, uint64_t* __restrict__ trace)
@@ -981,7 +984,9 @@ void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_b
     }
     if (kind == 0) {
         const uint32_t it = items[idx];
-        if ((it >> 24) == 8u) {             // up+WTA of frame f of wf
+        if constexpr (DPL > 16) {           // D > 256: no up+WTA items (host layout)
+            paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, it, lds_dyn64);
+        } else if ((it >> 24) == 8u) {      // up+WTA of frame f of wf
             using RC = RowsCfg<DPL>;
             const int f = (int)((it >> 22) & 3u);
             if (f < wf.n) {

@@ -297,8 +297,9 @@ struct Layout {
     size_t total = 0;
 };
 
-// Pipelined census batches fuse the upward vertical sweep with the WTA (census_sgm.hip
-// UpWta) unless SGM_UPWTA=0 (the earlier scheme: 8 volumes written, WTA rows interleaved).
+// Pipelined census batches with D <= 256 fuse the upward vertical sweep with the WTA
+// (census_sgm.hip UpWta) unless SGM_UPWTA=0 (the earlier scheme: 8 volumes written, WTA rows
+// interleaved).
 bool use_up_wta()
 {
     const char* e = std::getenv("SGM_UPWTA");
@@ -316,7 +317,9 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     if (p.mode == SGM_MODE_CENSUS8) {
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
         l.group = std::max(group, 1);
-        l.up_wta = group > 0 && use_up_wta();
+        // D > 256 (32 disparities per lane, 2 waves/SIMD) keeps the earlier scheme: its up+WTA
+        // blocks are long latency-bound chains (C5 batch: 32.3 vs 23.3 ms per frame)
+        l.up_wta = group > 0 && use_up_wta() && g.D <= 256;
         const int sets = group > 0 ? 2 * l.group : 1;
         for (int i = 0; i < sets; i++) l.vols[i] = take(l.vol_bytes * 8);
         for (int i = 0; i < (l.up_wta ? 3 * l.group : sets); i++) {
@@ -1538,6 +1541,28 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
         if (e_ != hipSuccess) return fail_band(b, e_, where); \
     } while (0)
     enum { EV_CENSUS = 0, EV_DOWN = 1, EV_UP = 2, EV_GATHER = 3 };
+    // SGM_TILE_TIMES=<file>: measurement mode — every band step runs alone (synchronised
+    // before and after) and its duration on the band's device is appended to the file as
+    // "band kind ms" lines (the per-band inputs of the multi-device critical-path model in
+    // DESIGN.md §7). Never set in production runs.
+    FILE* tt_file = nullptr;
+    if (const char* tf = std::getenv("SGM_TILE_TIMES")) tt_file = std::fopen(tf, "a");
+    hipEvent_t tt0 = nullptr, tt1 = nullptr;
+    auto tt_begin = [&](int b, hipStream_t s) {
+        if (!tt_file) return;
+        (void)hipSetDevice(h->bands[b]->device);
+        (void)hipDeviceSynchronize();
+        if (!tt0) { (void)hipEventCreate(&tt0); (void)hipEventCreate(&tt1); }
+        (void)hipEventRecord(tt0, s);
+    };
+    auto tt_end = [&](int b, const char* kind, hipStream_t s) {
+        if (!tt_file) return;
+        float ms = 0.f;
+        (void)hipEventRecord(tt1, s);
+        (void)hipEventSynchronize(tt1);
+        (void)hipEventElapsedTime(&ms, tt0, tt1);
+        std::fprintf(tt_file, "%d %s %.4f\n", b, kind, ms);
+    };
     // 1. inputs, census, horizontal scans (band-local)
     for (int b = 0; b < nb; b++) {
         sgm_handle* bh = h->bands[b];
@@ -1548,10 +1573,14 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
             std::memcpy(bh->pin + (size_t)y * W, L + (size_t)(e0 + y) * stride, W);
             std::memcpy(bh->pin + n + (size_t)y * W, R + (size_t)(e0 + y) * stride, W);
         }
+        tt_begin(b, bh->stream);
         BAND_TRY(b, hipMemcpyAsync(ws(b, bl[b].inL), bh->pin, n, hipMemcpyHostToDevice, bh->stream), "H2D");
         BAND_TRY(b, hipMemcpyAsync(ws(b, bl[b].inR), bh->pin + n, n, hipMemcpyHostToDevice, bh->stream), "H2D");
+        tt_end(b, "h2d", bh->stream);
+        tt_begin(b, bh->stream);
         BAND_TRY(b, sgm::launch_census((const uint8_t*)ws(b, bl[b].inL), (const uint8_t*)ws(b, bl[b].inR), W, W, He,
                                        (uint64_t*)ws(b, bl[b].cL), (uint64_t*)ws(b, bl[b].cR), bh->stream), "census");
+        tt_end(b, "census", bh->stream);
         BAND_TRY(b, hipEventRecord(bh->bev[EV_CENSUS], bh->stream), "event");
     }
     auto frames = [&](int b) {
@@ -1567,8 +1596,10 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
         for (int b = 0; b < nb; b++) {
             sgm_handle* bh = h->bands[b];
             BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
+            tt_begin(b, bh->stream);
             BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[0]),
                                                  bl[b].n_items[0], bh->stream), "horizontal paths");
+            tt_end(b, "horiz", bh->stream);
         }
         // 2. downward chain, top to bottom: band b continues band b-1's last row
         static const int down_dirs[3] = {0, 2, 3}, up_dirs[3] = {1, 4, 5};
@@ -1576,16 +1607,20 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
             sgm_handle* bh = h->bands[b];
             BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
             if (b > 0) BAND_TRY(b, hipStreamWaitEvent(bh->stream, h->bands[b - 1]->bev[EV_DOWN], 0), "wait");
+            tt_begin(b, bh->stream);
             BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[1]),
                                                  bl[b].n_items[1], bh->stream,
                                                  b > 0 ? (const uint8_t*)ws(b, bl[b].bnd[0]) : nullptr, nullptr,
                                                  bl[b].bnd_slot), "down paths");
+            tt_end(b, "down", bh->stream);
             if (b + 1 < nb) {
+                tt_begin(b, bh->stream);
                 const size_t last = (size_t)(g[b].H - 1) * cells_row;
                 for (int k = 0; k < 3; k++)
                     BAND_TRY(b, copy_between(ws(b + 1, bl[b + 1].bnd[0] + k * bl[b + 1].bnd_slot), h->bands[b + 1]->device,
                                              ws(b, bl[b].vols + down_dirs[k] * bl[b].vol_bytes + last), bh->device,
                                              cells_row, bh->stream), "boundary copy");
+                tt_end(b, "copy_down", bh->stream);
             }
             BAND_TRY(b, hipEventRecord(bh->bev[EV_DOWN], bh->stream), "event");
         }
@@ -1595,15 +1630,20 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
             BAND_TRY(b, hipSetDevice(bh->device), "hipSetDevice");
             BAND_TRY(b, hipStreamWaitEvent(bh->stream2, bh->bev[EV_CENSUS], 0), "wait");
             if (b + 1 < nb) BAND_TRY(b, hipStreamWaitEvent(bh->stream2, h->bands[b + 1]->bev[EV_UP], 0), "wait");
+            tt_begin(b, bh->stream2);
             BAND_TRY(b, sgm::launch_census_paths(frames(b), bl[b].vol_bytes, g[b], (const uint32_t*)ws(b, bl[b].items[2]),
                                                  bl[b].n_items[2], bh->stream2, nullptr,
                                                  b + 1 < nb ? (const uint8_t*)ws(b, bl[b].bnd[1]) : nullptr,
                                                  bl[b].bnd_slot), "up paths");
-            if (b > 0)
+            tt_end(b, "up", bh->stream2);
+            if (b > 0) {
+                tt_begin(b, bh->stream2);
                 for (int k = 0; k < 3; k++)
                     BAND_TRY(b, copy_between(ws(b - 1, bl[b - 1].bnd[1] + k * bl[b - 1].bnd_slot), h->bands[b - 1]->device,
                                              ws(b, bl[b].vols + up_dirs[k] * bl[b].vol_bytes), bh->device, cells_row,
                                              bh->stream2), "boundary copy");
+                tt_end(b, "copy_up", bh->stream2);
+            }
             BAND_TRY(b, hipEventRecord(bh->bev[EV_UP], bh->stream2), "event");
         }
     }
@@ -1616,12 +1656,16 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
             BAND_TRY(b, hipStreamWaitEvent(bh->stream, bh->bev[EV_UP], 0), "wait");
             sgm::WtaFrames wf{};
             wf.vols[0] = (const uint8_t*)ws(b, bl[b].vols); wf.out[0] = raw; wf.n = 1;
+            tt_begin(b, bh->stream);
             BAND_TRY(b, sgm::launch_census_wta(wf, bl[b].vol_bytes, g[b], W, bh->stream), "wta");
+            tt_end(b, "wta", bh->stream);
         } else {
             BAND_TRY(b, sgm::launch_fill16(raw, W, W, g[b].H, gf.invalid, bh->stream), "fill");
         }
+        tt_begin(b, bh->stream);
         BAND_TRY(b, copy_between(frame_raw + (size_t)c[b] * W, h->device, raw, bh->device, (size_t)W * g[b].H * 2,
                                  bh->stream), "gather");
+        tt_end(b, "gather", bh->stream);
         BAND_TRY(b, hipEventRecord(bh->bev[EV_GATHER], bh->stream), "event");
     }
 #undef BAND_TRY
@@ -1630,8 +1674,22 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
     for (int b = 0; b < nb; b++) HIP_TRY(hipStreamWaitEvent(h->stream, h->bands[b]->bev[EV_GATHER], 0), "wait");
     StageRec rec{h};
     int16_t* out = (int16_t*)(pws + pl.out);
+    if (tt_file) {
+        (void)hipDeviceSynchronize();
+        (void)hipEventRecord(tt0, h->stream);
+    }
     if ((rc = run_post(h, pl, gf, out, W, rec))) return rc;
     rec.end();
+    if (tt_file) {
+        float ms = 0.f;
+        (void)hipEventRecord(tt1, h->stream);
+        (void)hipEventSynchronize(tt1);
+        (void)hipEventElapsedTime(&ms, tt0, tt1);
+        std::fprintf(tt_file, "-1 post %.4f\n", ms);
+        (void)hipEventDestroy(tt0);
+        (void)hipEventDestroy(tt1);
+        std::fclose(tt_file);
+    }
     HIP_TRY(hipMemcpyAsync(h->pin, out, (size_t)W * H * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
     const int16_t* src = (const int16_t*)h->pin;

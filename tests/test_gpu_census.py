@@ -224,7 +224,7 @@ def test_device_batch_pipeline(engine, oracle, pkg, synth, monkeypatch, kw, n, u
     assert launches["census"] == min(n, 2)
     if n == 1:                # one frame: the single-frame pipeline (no group to fuse with)
         assert launches["paths8"] == 1 and launches["wta_lr"] == 1
-    elif up_wta:
+    elif up_wta and D <= 256:
         # census(G0) | fused[paths7(G0) + census(G1)] | fused[paths7(Gk) + upWTA(Gk-1) + census(Gk+1)]
         # rowfin ... | fused[paths8(Glast) + upWTA(Glast-1)] rowfin | wta(Glast)
         assert launches["wta_lr"] == 1 and launches.get("rowfin", 0) == ng - 1
