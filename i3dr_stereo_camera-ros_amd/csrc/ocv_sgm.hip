@@ -407,6 +407,7 @@ template <int LPL>
 __device__ __forceinline__ int line_shr1(int v, int p)
 {
     if constexpr (LPL == 16) return (int)row_shr1((uint32_t)v, (uint32_t)kMaxCost);
+    if constexpr (LPL == 64) return __builtin_amdgcn_update_dpp(kMaxCost, v, 0x138, 0xf, 0xf, false);   // lane 0: old
     const int t = __builtin_amdgcn_update_dpp(kMaxCost, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
     return p == 0 ? kMaxCost : t;                      // lane 32 must not see lane 31 (the other line)
 }
@@ -414,6 +415,7 @@ template <int LPL>
 __device__ __forceinline__ int line_shl1(int v, int p)
 {
     if constexpr (LPL == 16) return (int)row_shl1((uint32_t)v, (uint32_t)kMaxCost);
+    if constexpr (LPL == 64) return __builtin_amdgcn_update_dpp(kMaxCost, v, 0x130, 0xf, 0xf, false);   // lane 63: old
     const int t = __builtin_amdgcn_update_dpp(kMaxCost, v, 0x130, 0xf, 0xf, false);   // wave_shl:1
     return p == LPL - 1 ? kMaxCost : t;
 }
@@ -444,7 +446,8 @@ __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DP
 }
 
 // signed min over the LPL lanes of each line (16: a row; 32: a row pair joined by
-// v_permlane16_swap), result in every lane of the line
+// v_permlane16_swap; 64: the wave, halves joined by v_permlane32_swap), result in every
+// lane of the line
 template <int LPL>
 __device__ __forceinline__ int line_min_i32(int v)
 {
@@ -452,8 +455,12 @@ __device__ __forceinline__ int line_min_i32(int v)
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));     // quad_perm [2,3,0,1]
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, true));    // row_ror:4
     v = min(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, true));    // row_ror:8
-    if constexpr (LPL == 32) {
+    if constexpr (LPL >= 32) {
         const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // rows (0,1), (2,3) exchanged
+        v = min((int)sw[0], (int)sw[1]);
+    }
+    if constexpr (LPL == 64) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);   // halves exchanged
         v = min((int)sw[0], (int)sw[1]);
     }
     return v;
@@ -669,6 +676,75 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, 
     row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
+// WTA of the OCV modes for D > 512 (the node's cfg allows disparity ranges up to 2048):
+// one pixel per wave, 64 lanes x 16 disparities per chunk of 1024, chunks in turn. Pass 1
+// sums S (OpenCV's saturating order), keeps the key min over (S + 32768) * 2048 + d and
+// stores S in the wave's LDS slice; pass 2 reads the slice for the uniqueness test and
+// S[best +- 1]. Same decisions and the same disp2 / LR epilogue as k_ocv_wta16.
+constexpr int kWta64Chunk = 1024;
+template <int NDIR, typename VT>
+__global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, size_t vol_elems, Geom g,
+                                                   int16_t* __restrict__ out, size_t out_stride)
+{
+    if (ocv_gate_skip<VT>(g)) return;
+    constexpr int DPL = kWta64Chunk / 64;
+    extern __shared__ uint32_t lds_ocv[];
+    const int Dpad = (g.D + kWta64Chunk - 1) / kWta64Chunk * kWta64Chunk;
+    const int tid = threadIdx.x, lane = tid & 63, y = blockIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int16_t* srow = (int16_t*)lds_ocv + (size_t)w * Dpad;   // this wave's S slice
+    RowLds R((char*)lds_ocv + (size_t)4 * Dpad * 2, g.W);
+    R.init(g, tid, 256);
+    const int n = g.width1;
+    const size_t row0 = (size_t)y * g.width1 * g.D;
+    for (int x1 = w; x1 < n; x1 += 4) {
+        int km = 0x7FFFFFFF;
+        for (int c0 = 0; c0 < g.D; c0 += kWta64Chunk) {
+            const int db = c0 + lane * DPL;
+            const bool act = db < g.D;
+            const VT* base = vols + row0 + (size_t)x1 * g.D + (act ? db : 0);
+            int v[NDIR][DPL];
+#pragma unroll
+            for (int k = 0; k < NDIR; k++) load_vals<VT, DPL>(base + (size_t)k * vol_elems, v[k]);
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                int s1, s2;
+                if constexpr (NDIR == 5) {
+                    s1 = v[0][k] + v[1][k] + v[2][k] + v[3][k];
+                    s2 = v[4][k];
+                } else {
+                    s1 = v[0][k] + v[2][k] + v[3][k] + v[6][k];
+                    s2 = v[1][k] + v[4][k] + v[5][k] + v[7][k];
+                }
+                s1 = min(max(s1, -32768), 32767);
+                const int S = min(max(s1 + s2, -32768), 32767);
+                const int d = db + k;
+                const int key = ((S + 32768) << 11) | d;
+                km = (act && d < g.D) ? min(km, key) : km;
+                if (act) srow[d] = (int16_t)S;
+            }
+        }
+        const int kmin = wave_min(km);
+        const int best = kmin & 2047;
+        const int minS = (kmin >> 11) - 32768;
+        bool hit = false;
+        for (int d = lane; d < g.D; d += 64)
+            hit |= (unsigned)(d - best + 1) > 2u && (int)srow[d] * (100 - g.uniq) < minS * 100;
+        // every S saturated at MAX_COST: OpenCV's bestDisp stays -1 (see k_ocv_wta16)
+        const bool rej = __ballot(hit) != 0ull || minS >= 32767;
+        const int sm = srow[max(best - 1, 0)], sp = srow[min(best + 1, g.D - 1)];
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const bool wr = lane == 0;
+        const int x = wr ? g.minX1 + x1 : g.W + lane;
+        R.bst[x] = (int16_t)(rej ? -1 : best);
+        R.mins[x] = (uint16_t)minS;
+        R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
+    }
+    row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+}
+
 // ------------------------------------------------------------------------------------
 static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
@@ -734,6 +810,7 @@ constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lane
 static int ocv_lanes_per_line(const Geom& g, int dirmask)
 {
     if (g.D <= 32) return 16;
+    if (g.D > 512) return 64;       // a line per wave: 16 or 32 values per lane (D <= 2048)
     if (g.D > 256) return 32;       // 16 lanes x DPL 32 would straddle D when D % 32 = 16, and
                                     // its 32-value step is slower anyway (the shipped 2448x2048
                                     // D=480 config, MODE_SGBM paths: 17.4 ms vs 8.8 ms)
@@ -749,7 +826,11 @@ hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t cells, const Ge
                             hipStream_t st)
 {
     const int D = g.D;
-    if (ocv_lanes_per_line(g, dirmask) == 32) {
+    const int lpl = ocv_lanes_per_line(g, dirmask);
+    if (lpl == 64) {
+        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<32, 64>(C, vols, cells, g, dirmask, st);
+    } else if (lpl == 32) {
         if (D <= 64) launch_ocv_paths_v<2, 32>(C, vols, cells, g, dirmask, st);
         else if (D <= 128) launch_ocv_paths_v<4, 32>(C, vols, cells, g, dirmask, st);
         else if (D <= 256) launch_ocv_paths_v<8, 32>(C, vols, cells, g, dirmask, st);
@@ -784,6 +865,16 @@ static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geo
                              size_t out_stride, hipStream_t st)
 {
     const int D = g.D;
+    if (D > 512) {
+        const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
+        const size_t lds = (size_t)4 * ((D + kWta64Chunk - 1) / kWta64Chunk * kWta64Chunk) * 2 + RowLds::bytes(g.W);
+        const VT* v = (const VT*)vols;
+        if (ndir == 8)
+            hipLaunchKernelGGL((k_ocv_wta64<8, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        else
+            hipLaunchKernelGGL((k_ocv_wta64<5, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        return;
+    }
     if (D <= 32) launch_ocv_wta_dpl<2, VT>(vols, cells, ndir, g, out, out_stride, st);
     else if (D <= 64) launch_ocv_wta_dpl<4, VT>(vols, cells, ndir, g, out, out_stride, st);
     else if (D <= 128) launch_ocv_wta_dpl<8, VT>(vols, cells, ndir, g, out, out_stride, st);

@@ -68,7 +68,14 @@ int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
         err = "numDisparities must be a positive multiple of 16 (OpenCV: CV_Assert(D % 16 == 0))";
         return SGM_ERR_PARAM;
     }
-    if (p.num_disparities > 512) { err = "numDisparities > 512 is not supported by this build"; return SGM_ERR_UNSUPPORTED; }
+    // OCV modes: up to 2048 (the node's cfg range, i3DR_Disparity.cfg:27); census mode: 512
+    // (its u8 path engine keeps at most 32 disparities per lane of a 16-lane line)
+    const int max_d = p.mode == SGM_MODE_CENSUS8 ? 512 : 2048;
+    if (p.num_disparities > max_d) {
+        err = p.mode == SGM_MODE_CENSUS8 ? "numDisparities > 512 is not supported in the census mode"
+                                         : "numDisparities > 2048 is not supported";
+        return SGM_ERR_UNSUPPORTED;
+    }
     g = Geom{};
     g.W = W; g.H = H;
     g.minD = p.min_disparity; g.D = p.num_disparities;

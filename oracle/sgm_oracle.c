@@ -126,7 +126,8 @@ static int effective(const sgm_params* p, int width, int height, eff_t* e)
     e->maxX1 = width + imin(e->minD, 0);
     e->width1 = e->maxX1 - e->minX1;
     e->invalid_scaled = (e->minD - 1) * DISP_SCALE;
-    if (e->D > 512) return SGM_ERR_UNSUPPORTED;
+    /* the engine's limits: census 512 (u8 path engine), OpenCV modes 2048 (the node's cfg) */
+    if (e->D > (e->census ? 512 : 2048)) return SGM_ERR_UNSUPPORTED;
     if (width > 32767 || height > 32767) return SGM_ERR_UNSUPPORTED;
     return SGM_OK;
 }

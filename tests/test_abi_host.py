@@ -49,10 +49,14 @@ def test_default_params_match_node_defaults(pkg):
     assert (c.p1, c.p2, c.uniqueness_ratio, c.subpixel, c.lr_check) == (10, 120, 5, 1, 1)
 
 
-@pytest.mark.parametrize("D,expect", [(64, 0), (24, -2), (0, -2), (528, -5), (512, 0)])
-def test_check_params(pkg, D, expect):
+@pytest.mark.parametrize("mode,D,expect", [("census", 64, 0), ("census", 24, -2), ("census", 0, -2),
+                                           ("census", 528, -5), ("census", 512, 0),
+                                           ("ocv", 528, 0), ("ocv", 2048, 0), ("ocv", 2064, -5), ("ocv", 40, -2)])
+def test_check_params(pkg, mode, D, expect):
+    """D limits: census 512 (u8 path engine); the OpenCV modes 2048, the top of the node's
+    cfg range (cfg/i3DR_Disparity.cfg:27, disparity_range <= 2056 rounded down to x16)."""
     lib = pkg.load_library()
-    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D)
+    p = pkg.default_params(pkg.MODE_CENSUS8 if mode == "census" else pkg.MODE_OCV_SGBM5, num_disparities=D)
     assert lib.sgm_check_params(ctypes.byref(p), 640, 480) == expect
 
 

@@ -198,3 +198,21 @@ def test_plugin_core_cpp_init_and_match(tmp_path, oracle, synth):
     assert r.returncode == 0, r.stderr
     got = np.fromfile(op, np.float32).reshape(96, 256)
     assert np.array_equal(got, oracle.match(oracle.make_params(0), left, right).astype(np.float32))
+
+
+@pytest.mark.parametrize("wide", ["", "1"], ids=["int16", "int32"])
+@pytest.mark.parametrize("mode,h,w,minD,D,block,spk", [(0, 20, 1400, 0, 1024, 5, 100), (1, 24, 1300, -7, 784, 3, 0),
+                                                       (0, 12, 2300, 3, 2048, 7, 0), (1, 28, 2200, 0, 1536, 5, 0)])
+def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wide, mode, h, w, minD, D, block, spk):
+    """D > 512 in the OpenCV modes (the node's cfg allows disparity ranges up to 2048):
+    64-lane path lines (16 or 32 values per lane) and the one-pixel-per-wave WTA in chunks of
+    1024 disparities, int16 and int32 (SGM_OCV_WIDE) volumes."""
+    if wide:
+        monkeypatch.setenv("SGM_OCV_WIDE", wide)
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), min(D, 256), seed=D + h)
+    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, speckle_window_size=spk)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    assert (ref[:, max(minD + D, 0):] != (minD - 1) * 16).any()      # some matched pixels to compare
