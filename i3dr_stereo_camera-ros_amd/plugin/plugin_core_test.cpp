@@ -4,6 +4,10 @@
 // Modes:  plugin_core_test init              (the warm-up; needs a GPU)
 //         plugin_core_test setters           (setter semantics; no GPU)
 //         plugin_core_test match <L.raw> <R.raw> <W> <H> <out.f32> [algo params...]
+//         plugin_core_test time <L.raw> <R.raw> <W> <H> <algo> <D> <minD> <block> <reps>
+//                          (ms per forwardMatch: the node's host-buffer call, float output)
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -69,6 +73,33 @@ int main(int argc, char** argv)
         std::vector<float> d((size_t)W * H);
         if (m.forwardMatch(L.data(), R.data(), W, H, W, d.data(), W) != 0) return fail("match");
         std::ofstream(argv[6], std::ios::binary).write((const char*)d.data(), d.size() * sizeof(float));
+        return 0;
+    }
+    if (!std::strcmp(mode, "time") && argc >= 11) {
+        const int W = std::atoi(argv[4]), H = std::atoi(argv[5]), reps = std::max(std::atoi(argv[10]), 1);
+        std::vector<uint8_t> L((size_t)W * H), R((size_t)W * H);
+        std::ifstream(argv[2], std::ios::binary).read((char*)L.data(), L.size());
+        std::ifstream(argv[3], std::ios::binary).read((char*)R.data(), R.size());
+        sgm_hip::MatcherCore m(0, std::atoi(argv[6]));
+        m.setDisparityRange(std::atoi(argv[7]), W);
+        m.setMinDisparity(std::atoi(argv[8]));
+        m.setWindowSize(std::atoi(argv[9]));
+        m.setUniquenessRatio(15);
+        m.setSpeckleFilterRange(4);
+        m.setSpeckleFilterWindow(100);
+        m.setPreFilterCap(31);
+        m.setP1(200);
+        m.setP2(400);
+        std::vector<float> d((size_t)W * H);
+        if (m.forwardMatch(L.data(), R.data(), W, H, W, d.data(), W) != 0) return fail("match");   // warm-up
+        std::vector<double> t;
+        for (int i = 0; i < reps; i++) {
+            const auto a = std::chrono::steady_clock::now();
+            if (m.forwardMatch(L.data(), R.data(), W, H, W, d.data(), W) != 0) return fail("match");
+            t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count());
+        }
+        std::sort(t.begin(), t.end());
+        std::printf("{\"ms_median\": %.4f, \"ms_min\": %.4f, \"reps\": %d}\n", t[t.size() / 2], t[0], reps);
         return 0;
     }
     return fail("usage");
