@@ -252,6 +252,30 @@ def main():
 
     elapsed_max = max_over_ranks(elapsed, device)
 
+    # single-frame latency beside the batch throughput (BASELINE's C2 is quoted as a single
+    # frame): one sgm_match_device per frame on resident buffers, HIP events on the stream
+    single = None
+    if rank == 0 and not args.host_io:
+        reps = 10
+        one = lambda i: eng.match_device(ptr_l[i % len(ptr_l)], ptr_r[i % len(ptr_r)], W, H, W, ptr_o[i % len(ptr_o)],
+                                         W, stream)
+        one(0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(tstream)
+        for i in range(reps):
+            one(i)
+        e1.record(tstream)
+        torch.cuda.synchronize()
+        eng.set_profiling(True)          # per-stage split in a separate pass
+        for i in range(reps):
+            one(i)
+        torch.cuda.synchronize()
+        single = {"ms": round(e0.elapsed_time(e1) / reps, 4), "pairs_per_s": round(1000.0 * reps / e0.elapsed_time(e1), 1),
+                  "stages": {n: round(ms, 4) for n, ms, _ in eng.stage_times()},
+                  "note": "one frame per sgm_match_device call (census -> 8 directions -> WTA), no batching"}
+        eng.set_profiling(False)
+
     frames_total = args.frames * args.steps * world
     value = frames_total / elapsed_max
     ms_per_step = elapsed_max * 1e3 / args.steps
@@ -314,6 +338,7 @@ def main():
             "stages": [{"name": n, "avg_ms": round(ms, 5), "launches": launches[n], "alg_bytes": b,
                         "GBps": round(b / (ms * 1e-3) / 1e9, 1)} for n, ms, b in stages],
             "profiled_frames": n_prof,
+            "single_frame": single,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg)
