@@ -345,6 +345,7 @@ def main():
         print(json.dumps(res))
     eng.close()
     if distributed:
+        dist.barrier()              # rank 0's single-frame / CPU legs end before the group does
         dist.destroy_process_group()
 
 
