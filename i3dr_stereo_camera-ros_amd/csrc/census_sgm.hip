@@ -616,8 +616,15 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
             const WtaPix px = wta_pix16<DPL, EXACT>(E, O, p, g, inv_u, srow);
             const uint64_t v = (uint64_t)(uint16_t)(px.rej ? g.invalid : px.d16) |
                                ((uint64_t)(uint16_t)(px.rej ? -1 : px.best) << 16) | ((uint64_t)(uint16_t)px.minS << 32);
-            uint64_t* dst = (valid && p == 0) ? uw.res + (size_t)y * g.W + x : uw.res + (size_t)g.W * g.H + lane;
-            __builtin_nontemporal_store(v, dst);
+            // lane 0 of each line stores its pixel; the other lanes' stores go past the row
+            // descriptor's range, where the hardware drops them (no branch, and no trash slot:
+            // 60 of 64 lanes storing into one shared 512-B slot every step made all the frames'
+            // up+WTA waves contend on the same lines — 3 frames per launch ran 5x slower)
+            const __amdgpu_buffer_rsrc_t rr =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(uw.res + (size_t)y * g.W), 0, g.W * 8, 0x00020000);
+            typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), rr,
+                                                  (valid && p == 0) ? (uint32_t)x * 8u : 0x80000000u, 0, 2);
         } else {
             const bool ok = valid && lane_act && !((SGM_EXP & 2) && dir == 1);
             uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;

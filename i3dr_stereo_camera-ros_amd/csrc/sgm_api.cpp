@@ -323,6 +323,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
     if (p.mode == SGM_MODE_CENSUS8) {
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
+        if (const char* e = std::getenv("SGM_VOL_PAD")) l.vol_bytes = align_up(l.vol_bytes + (size_t)std::atoll(e));
         l.group = std::max(group, 1);
         // D > 256 (32 disparities per lane, 2 waves/SIMD) keeps the earlier scheme: its up+WTA
         // blocks are long latency-bound chains (C5 batch: 32.3 vs 23.3 ms per frame)
