@@ -69,6 +69,26 @@ def load_pmc_traffic(config):
         return None
 
 
+def hbm_copy_gbps(device, nbytes=2 << 30, reps=5):
+    """Achievable HBM copy bandwidth on this GPU (reported beside the 8 TB/s
+    spec peak): a device-to-device copy of `nbytes`, read + write bytes counted."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbps, 1)
+
+
 def cpu_baseline(cfg, budget_s=20.0):
     """Times the CPU port of the same workload (oracle, multi-threaded C) on host cores."""
     import numpy as np
@@ -82,6 +102,11 @@ def cpu_baseline(cfg, budget_s=20.0):
     p = orc.make_params(orc.MODE_CENSUS8, num_disparities=cfg["D"], subpixel=cfg["subpixel"],
                         lr_check=cfg["lr_check"])
     threads = orc.num_threads()
+    cpu_model = ""
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     n, t0 = 0, time.perf_counter()
     while True:
         orc.match(p, left, right)
@@ -89,7 +114,8 @@ def cpu_baseline(cfg, budget_s=20.0):
         if time.perf_counter() - t0 > budget_s / 2 or n >= 8:
             break
     dt = time.perf_counter() - t0
-    out = {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+    out = {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port", "cpu_model": cpu_model,
+           "host_cpus_visible": os.cpu_count(),
            "sample": f"{n} full {cfg['w']}x{cfg['h']} D={cfg['D']} frames of the same census-SGM workload, "
                      f"oracle/sgm_oracle.c (OpenMP over lines, {threads} threads)"}
     # the reference's own CPU path: OpenCV-SGBM restatement, single thread, same geometry
@@ -306,7 +332,9 @@ def main():
                 traffic_profile = {"hbm_bytes_per_launch": pmc["kernels"][dom[0]].get("hbm_bytes_per_launch"),
                                    "source": f"profiles/latest_pmc_{args.config}.json (rocprofv3 --pmc, separate run; "
                                              "tools/refresh_profiles.sh)", "git": pmc.get("git")}
+            copy_gbps = hbm_copy_gbps(device)
             roofline = {"bound": "hbm", "kernel": dom[0], "achieved": round(dom_achieved, 1),
+                        "measured_copy_GBps": copy_gbps,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(dom_achieved / HBM_PEAK_GBS, 4),
                         "traffic": None, "traffic_profile": traffic_profile,
                         "algorithmic_bytes_per_launch": dom_bytes,
