@@ -216,3 +216,15 @@ def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wid
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
     assert (ref[:, max(minD + D, 0):] != (minD - 1) * 16).any()      # some matched pixels to compare
+
+
+@pytest.mark.parametrize("block", [61, 63, 65, 131])
+def test_ocv_tall_boxes(engine, oracle, synth, pkg, block):
+    """Tall SAD boxes (the cfg allows windows up to 255): the fused pixel-cost + box kernel
+    up to its 64 KB tile, the unfused pixcost + hsum pair beyond it, long vertical windows."""
+    left, right, _ = synth.stereo_pair(150, 320, 0, 32, seed=block)
+    p = pkg.default_params(0, min_disparity=0, num_disparities=32, block_size=block, speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
