@@ -102,91 +102,110 @@ __global__ __launch_bounds__(256) void k_ocv_hsum(const int16_t* __restrict__ pi
 }
 
 // Pixel cost + horizontal SAD box fused: one block per XB output pixels x DC disparities of
-// a row (blockIdx.z: the disparity chunk). The BT intervals of both images and the pixel
-// costs of the XB + 2*SW2 columns the box reads (positions clamped to [0, width1), as the
-// running sum's replicate rule) live in LDS; the box is a direct (2*SW2+1)-term sum of them —
-// the same integer as the running sum. Chunking the disparities lets a block take many
-// output columns (few halo columns recomputed) at any D: the shipped 2448x2048 D=480 block-21
-// config went 5.38 -> see DESIGN (XB 32 x all 480 d: 52 staged columns per 32 outputs, 51 KB).
+// a row (blockIdx.z: the disparity chunk). Chunking the disparities lets a block take many
+// output columns (few halo columns recomputed) at any D: with all D in one block it could
+// take only 32 columns, and a 21-wide box recomputed 52 columns per 32 outputs (the shipped
+// 2448x2048 D=480 block-21 config: 5.38 -> 3.38 ms).
+//   stage:  the Birchfield-Tomasi intervals (u, lo, hi) of both channels of the NX = XB + 2*SW2
+//           left columns and of the NR = NX + DC - 1 right columns they meet, as u16 planes
+//           (the right ones twice, the second copy shifted by one, so a 32-bit read at either
+//           parity returns two adjacent entries);
+//   cost:   P[d][k] for column pairs (k, k+1): the pair's left and right entries are adjacent
+//           (r = k + DC - 1 - d), so one u32 read per plane and packed i16 arithmetic give two
+//           cells (≈10 packed ops and 3 LDS reads per cell, was ≈33 VALU and 13 LDS);
+//   box:    thread (segment, d) slides its window over the segment's outputs, 2 LDS reads per
+//           output; columns outside [0, width1) read the edge column (the running sum's
+//           replicate rule).
 constexpr int kPixXB = 128;     // output columns per block
 constexpr int kPixDC = 128;     // disparities per block
 __host__ __device__ inline int pix_xb(const Geom& g) { return g.D >= kPixDC ? kPixXB : kPixXB * 2; }
 __host__ __device__ inline int pix_dc(const Geom& g) { return g.D < kPixDC ? g.D : kPixDC; }
-__host__ inline size_t pix_lds_bytes(const Geom& g)
-{
-    const int XB = pix_xb(g), DC = pix_dc(g), NX = XB + 2 * g.SW2;
-    return (((size_t)2 * NX * DC + 7) & ~(size_t)7) + 8 * NX + 8 * (NX + DC - 1);
-}
+struct PixGeo {
+    int XB, DC, NX, NR, NXP;    // NX even; NXP: P's row pitch in u16, NXP/2 odd (conflict-free columns)
+    __host__ __device__ PixGeo(const Geom& g) {
+        XB = pix_xb(g); DC = pix_dc(g);
+        NX = (XB + 2 * g.SW2 + 1) & ~1;
+        NR = (NX + DC) & ~1;                        // >= NX + DC - 1 entries, even
+        NXP = (NX / 2) % 2 ? NX : NX + 2;
+    }
+    __host__ __device__ size_t bytes() const { return (size_t)2 * ((size_t)DC * NXP + 6 * NX + 12 * (NR + 2)); }
+};
+__host__ inline size_t pix_lds_bytes(const Geom& g) { return PixGeo(g).bytes(); }
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__ planes, Geom g,
                                                      int16_t* __restrict__ hs)
 {
-    extern __shared__ uint8_t lds_pix[];
-    const int XB = pix_xb(g), DCmax = pix_dc(g);
+    extern __shared__ uint32_t lds_pix32[];
+    const PixGeo pg(g);
+    const int XB = pg.XB, DCmax = pg.DC, NX = pg.NX, NR = pg.NR, NXP = pg.NXP;
     const int y = blockIdx.y, x0 = blockIdx.x * XB, tid = threadIdx.x;
     const int d0 = blockIdx.z * DCmax, DC = min(DCmax, g.D - d0);
-    const int SW2 = g.SW2, NX = XB + 2 * SW2;              // pixel-cost columns staged
-    const int NR = NX + DC - 1;                            // right-image BT entries needed
+    const int SW2 = g.SW2;
     const size_t plane = (size_t)g.W * g.H;
-    int16_t* P = (int16_t*)lds_pix;                        // [NX][DC]
-    // BT intervals as 8-byte records (u, lo, hi of channel 0, then of channel 1, 2 pad):
-    // a cell's six reads per side share one address (immediate offsets), which matters
-    // because this kernel is VALU-bound (one address add per read otherwise)
-    uint8_t* bl = lds_pix + (((size_t)2 * NX * DC + 7) & ~(size_t)7);   // left  [NX] records
-    uint8_t* br = bl + 8 * NX;                                          // right [NR] records
-    // staged column i -> x1 = clamp(x0 - SW2 + i); right entry r -> xr = xlo - minD - (d0+DC-1) + r
-    const int xlo = g.minX1 + min(max(x0 - SW2, 0), g.width1 - 1);
+    uint16_t* P = (uint16_t*)lds_pix32;                    // [DCmax][NXP]
+    uint16_t* Lp = P + (size_t)DCmax * NXP;                // 6 planes x NX: (u, lo, hi) of channel 0, then 1
+    uint16_t* Rp = Lp + 6 * NX;                            // 6 planes x (NR + 2)
+    uint16_t* Rs = Rp + 6 * (NR + 2);                      // the same shifted by one entry
+    // staged column k <-> x = minX1 + x0 - SW2 + k (not clamped: out-of-frame columns get
+    // clamped BT entries and are never summed); right entry r <-> xr = x(0) - minD - (d0 + DC - 1) + r
+    const int xs = g.minX1 + x0 - SW2;
     for (int i = tid; i < 2 * NX; i += 256) {
         const int c = i / NX, k = i - c * NX;
-        const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
         int u, lo, hi;
-        bt_lohi(planes + c * plane + (size_t)y * g.W, x, g.W, u, lo, hi);
-        bl[8 * k + 3 * c] = (uint8_t)u; bl[8 * k + 3 * c + 1] = (uint8_t)lo; bl[8 * k + 3 * c + 2] = (uint8_t)hi;
+        bt_lohi(planes + c * plane + (size_t)y * g.W, min(max(xs + k, 0), g.W - 1), g.W, u, lo, hi);
+        Lp[(3 * c) * NX + k] = (uint16_t)u; Lp[(3 * c + 1) * NX + k] = (uint16_t)lo; Lp[(3 * c + 2) * NX + k] = (uint16_t)hi;
     }
-    const int xr0 = xlo - g.minD - (d0 + DC - 1);
-    for (int i = tid; i < 2 * NR; i += 256) {
-        const int c = i / NR, r = i - c * NR;
-        const int xr = min(max(xr0 + r, 0), g.W - 1);
+    const int xr0 = xs - g.minD - (d0 + DC - 1);
+    for (int i = tid; i < 2 * (NR + 1); i += 256) {
+        const int c = i / (NR + 1), r = i - c * (NR + 1);
         int v, lo, hi;
-        bt_lohi(planes + (2 + c) * plane + (size_t)y * g.W, xr, g.W, v, lo, hi);
-        br[8 * r + 3 * c] = (uint8_t)v; br[8 * r + 3 * c + 1] = (uint8_t)lo; br[8 * r + 3 * c + 2] = (uint8_t)hi;
+        bt_lohi(planes + (2 + c) * plane + (size_t)y * g.W, min(max(xr0 + r, 0), g.W - 1), g.W, v, lo, hi);
+        const int q = 3 * c * (NR + 2);
+        Rp[q + r] = (uint16_t)v; Rp[q + (NR + 2) + r] = (uint16_t)lo; Rp[q + 2 * (NR + 2) + r] = (uint16_t)hi;
+        if (r > 0) { Rs[q + r - 1] = (uint16_t)v; Rs[q + (NR + 2) + r - 1] = (uint16_t)lo; Rs[q + 2 * (NR + 2) + r - 1] = (uint16_t)hi; }
     }
     __syncthreads();
-    // (k, d) of flat index i = k * DC + d, advanced by 256 per iteration without divisions
-    const int kstep = 256 / DC, dstep = 256 - kstep * DC;
-    int k = tid / DC, d = tid - k * DC;
-    for (int i = tid; i < NX * DC; i += 256) {
-        const int x = g.minX1 + min(max(x0 - SW2 + k, 0), g.width1 - 1);
-        const uint8_t* L8 = bl + 8 * k;
-        const uint8_t* R8 = br + 8 * (x - g.minD - (d0 + d) - xr0);   // entry of xr = x - minD - d
-        int acc = 0;
+    // thread -> disparity d (fixed), column pairs kp, kp + step, ...
+    const int npair = NX / 2, tpd = 256 / DCmax;           // threads per disparity
+    const int d = tid % DCmax, kp0 = tid / DCmax;
+    if (d < DC && kp0 < tpd) {
+        const int roff = DC - 1 - d;                       // r = k + roff
+        const uint16_t* R = (roff & 1) ? Rs + (roff - 1) : Rp + roff;   // u32-aligned for every even k
+        auto rd = [&](const uint16_t* base, int off) { return __builtin_bit_cast(s16x2_t, *(const uint32_t*)(base + off)); };
+        const s16x2_t zero = {0, 0};
+        for (int kp = kp0; kp < npair; kp += tpd) {
+            const int k = 2 * kp;
+            s16x2_t acc = zero;
 #pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const int u = L8[3 * c], ulo = L8[3 * c + 1], uhi = L8[3 * c + 2];
-            const int v = R8[3 * c], v0 = R8[3 * c + 1], v1 = R8[3 * c + 2];
-            const int c0 = max(0, max(u - v1, v0 - u));
-            const int c1 = max(0, max(v - uhi, ulo - v));
-            acc += min(c0, c1) >> (c == 0 ? 0 : 2);
+            for (int c = 0; c < 2; c++) {
+                const s16x2_t u = rd(Lp, (3 * c) * NX + k), ulo = rd(Lp, (3 * c + 1) * NX + k), uhi = rd(Lp, (3 * c + 2) * NX + k);
+                const int q = 3 * c * (NR + 2);
+                const s16x2_t v = rd(R, q + k), v0 = rd(R, q + (NR + 2) + k), v1 = rd(R, q + 2 * (NR + 2) + k);
+                const s16x2_t c0 = __builtin_elementwise_max(__builtin_elementwise_max(u - v1, v0 - u), zero);
+                const s16x2_t c1 = __builtin_elementwise_max(__builtin_elementwise_max(v - uhi, ulo - v), zero);
+                const s16x2_t m = __builtin_elementwise_min(c0, c1);
+                acc += c == 0 ? m : (m >> (s16x2_t){2, 2});
+            }
+            *(uint32_t*)(P + (size_t)d * NXP + k) = __builtin_bit_cast(uint32_t, acc);
         }
-        P[i] = (int16_t)acc;
-        k += kstep; d += dstep;
-        if (d >= DC) { d -= DC; k++; }
     }
     __syncthreads();
     // horizontal box: thread (segment, d) slides its window over the segment's outputs
-    // (2 LDS reads per output after the first; int sums, so any order is exact)
     const int nout = min(XB, g.width1 - x0);
+    const int klo = SW2 - x0, khi = g.width1 - 1 - x0 + SW2;   // staged columns inside [0, width1)
+    auto pk = [&](const uint16_t* Pd, int k) { return (int)(int16_t)Pd[min(max(k, klo), khi)]; };
     int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D + d0;
     const int nseg = max(256 / DC, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
     for (int t = tid; t < nseg * DC; t += 256) {
         const int seg = t / DC, dd = t - seg * DC;
         const int xa = seg * seglen, xb = min(xa + seglen, nout);
         if (xa >= xb) continue;
-        const int16_t* Pd = P + dd;
+        const uint16_t* Pd = P + (size_t)dd * NXP;
         int sum = 0;
-        for (int u = 0; u <= BW; u++) sum += Pd[(xa + u) * DC];
+        for (int u = 0; u <= BW; u++) sum += pk(Pd, xa + u);
         dst[(size_t)xa * g.D + dd] = (int16_t)sum;
         for (int xo = xa + 1; xo < xb; xo++) {
-            sum += Pd[(xo + BW) * DC] - Pd[(xo - 1) * DC];
+            sum += pk(Pd, xo + BW) - pk(Pd, xo - 1);
             dst[(size_t)xo * g.D + dd] = (int16_t)sum;
         }
     }
