@@ -43,7 +43,7 @@ EXPORTS = [
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
     "sgm_remap_cubic", "sgm_cubic_table", "sgm_set_rectification", "sgm_match_device_batch_rect", "sgm_debug_census",
-    "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle",
+    "sgm_debug_census_path", "sgm_debug_ocv_cost", "sgm_debug_median3", "sgm_debug_speckle", "sgm_debug_path_items",
 ]
 
 
@@ -131,6 +131,7 @@ def load_library(path=None):
     L.sgm_debug_ocv_cost.argtypes = [vp, vp, vp, ci, ci, sz, vp]
     L.sgm_debug_median3.argtypes = [vp, vp, ci, ci]
     L.sgm_debug_speckle.argtypes = [vp, vp, ci, ci, ci, ci, ci]
+    L.sgm_debug_path_items.argtypes = [P(SgmParams), ci, ci, ctypes.c_uint, ci, ci, ci, vp, ci]
     _lib = L
     return L
 

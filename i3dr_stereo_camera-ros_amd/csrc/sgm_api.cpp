@@ -1881,6 +1881,21 @@ static int debug_post(sgm_handle* h, int16_t* disp, int W, int H, int which, int
 
 int sgm_debug_median3(sgm_handle* h, int16_t* disp, int W, int H) { return debug_post(h, disp, W, H, 0, 0, 0, 0); }
 
+int sgm_debug_path_items(const sgm_params* p, int width, int height, unsigned dir_mask, int n_slots, int group,
+                         int up_group, uint32_t* out, int cap)
+{
+    if (!p || p->mode != SGM_MODE_CENSUS8) return SGM_ERR_ARG;
+    Geom g;
+    std::string err;
+    const int rc = make_geom(*p, width, height, g, err);
+    if (rc) return rc;
+    if (g.width1 <= 0) return 0;
+    const int n = sgm::census_path_items(g, dir_mask & 0xFFu, n_slots, group, nullptr, 0, up_group);
+    if (!out) return n;
+    if (n > cap) return SGM_ERR_ARG;
+    return sgm::census_path_items(g, dir_mask & 0xFFu, n_slots, group, out, cap, up_group);
+}
+
 int sgm_debug_speckle(sgm_handle* h, int16_t* disp, int W, int H, int new_val, int max_size, int max_diff)
 {
     return debug_post(h, disp, W, H, 1, new_val, max_size, max_diff);

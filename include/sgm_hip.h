@@ -254,6 +254,13 @@ int  sgm_debug_census_path(sgm_handle* h, const uint8_t* left, const uint8_t* ri
  * layout [H][width1][D].                                                                  */
 int  sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* left, const uint8_t* right,
                         int width, int height, size_t stride, int16_t* cost);
+/* Census mode: the path work list one launch would dispatch (host-only, no device): every
+ * 16-line block of the directions in dir_mask (bit d) of `group` frames, plus the up+WTA
+ * blocks (code 8) of `up_group` frames, as dir << 24 | frame << 22 | block, longest first,
+ * dealt in a snake over rounds of n_slots. Returns the entry count (out may be NULL), or
+ * < 0 on an error (cap too small: SGM_ERR_ARG).                                           */
+int  sgm_debug_path_items(const sgm_params* p, int width, int height, unsigned dir_mask, int n_slots,
+                          int group, int up_group, uint32_t* out, int cap);
 /* 3x3 median (replicate border) and speckle filter on a host int16 image, in place.       */
 int  sgm_debug_median3(sgm_handle* h, int16_t* disp, int width, int height);
 int  sgm_debug_speckle(sgm_handle* h, int16_t* disp, int width, int height,
