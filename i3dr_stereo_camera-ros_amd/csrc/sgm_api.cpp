@@ -1553,9 +1553,19 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
     // before and after) and its duration on the band's device is appended to the file as
     // "band kind ms" lines (the per-band inputs of the multi-device critical-path model in
     // DESIGN.md §7). Never set in production runs.
-    FILE* tt_file = nullptr;
-    if (const char* tf = std::getenv("SGM_TILE_TIMES")) tt_file = std::fopen(tf, "a");
-    hipEvent_t tt0 = nullptr, tt1 = nullptr;
+    struct TileTimes {           // closed / destroyed on every return path
+        FILE* f = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~TileTimes() {
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            if (f) std::fclose(f);
+        }
+    } tt;
+    if (const char* tf = std::getenv("SGM_TILE_TIMES")) tt.f = std::fopen(tf, "a");
+    FILE*& tt_file = tt.f;
+    hipEvent_t& tt0 = tt.e0;
+    hipEvent_t& tt1 = tt.e1;
     auto tt_begin = [&](int b, hipStream_t s) {
         if (!tt_file) return;
         (void)hipSetDevice(h->bands[b]->device);
@@ -1694,9 +1704,6 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
         (void)hipEventSynchronize(tt1);
         (void)hipEventElapsedTime(&ms, tt0, tt1);
         std::fprintf(tt_file, "-1 post %.4f\n", ms);
-        (void)hipEventDestroy(tt0);
-        (void)hipEventDestroy(tt1);
-        std::fclose(tt_file);
     }
     HIP_TRY(hipMemcpyAsync(h->pin, out, (size_t)W * H * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
