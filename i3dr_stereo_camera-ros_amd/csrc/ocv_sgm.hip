@@ -543,7 +543,11 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     constexpr int PF = DPL <= 4 ? SGM_OCV_PF : SGM_OCV_PF_WIDE;
     int Cb[PF][DPL];
     const bool lane_act = p * DPL < g.D;
-    const int dl = min(p * DPL, g.D - DPL);
+    // 32 values per lane (64-lane lines, D > 1024) with D % 32 = 16: one lane straddles D. It
+    // loads from its own first d (its upper 16 values read the next cell: d >= D never reaches
+    // a valid entry) and stores only its lower half. Lanes wholly past D load the last group.
+    const bool straddle = DPL == 32 && lane_act && p * DPL + DPL > g.D;
+    const int dl = lane_act ? p * DPL : g.D - DPL;
     // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop).
     // The first PF steps are peeled (pv = false only at step 0, a constant elsewhere).
     if (use_buf) {
@@ -566,7 +570,15 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                 const int i = i0 + q;
                 int L[DPL], Lraw[DPL];
                 const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
-                bstore_vals<VT, DPL>(rsV, lane_act && i < n ? st_b : 0x80000000u, kRaw ? Lraw : L);
+                const bool ok = lane_act && i < n;
+                if constexpr (DPL == 32) {        // two halves: the straddling lane drops its upper one
+                    const int (&Vs)[32] = kRaw ? Lraw : L;
+                    bstore_vals<VT, 16>(rsV, ok ? st_b : 0x80000000u, *reinterpret_cast<const int(*)[16]>(&Vs[0]));
+                    bstore_vals<VT, 16>(rsV, ok && !straddle ? st_b + 16u * (uint32_t)sizeof(VT) : 0x80000000u,
+                                        *reinterpret_cast<const int(*)[16]>(&Vs[16]));
+                } else {
+                    bstore_vals<VT, DPL>(rsV, ok ? st_b : 0x80000000u, kRaw ? Lraw : L);
+                }
                 mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];
@@ -596,7 +608,14 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                 int L[DPL], Lraw[DPL];
                 const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
                 const bool ok = lane_act && i < n;
-                store_vals<VT, DPL>(ok ? V + cell(i) + dl : tr, kRaw ? Lraw : L);
+                if constexpr (DPL == 32) {
+                    const int (&Vs)[32] = kRaw ? Lraw : L;
+                    store_vals<VT, 16>(ok ? V + cell(i) + dl : tr, *reinterpret_cast<const int(*)[16]>(&Vs[0]));
+                    store_vals<VT, 16>(ok && !straddle ? V + cell(i) + dl + 16 : tr + 16,
+                                       *reinterpret_cast<const int(*)[16]>(&Vs[16]));
+                } else {
+                    store_vals<VT, DPL>(ok ? V + cell(i) + dl : tr, kRaw ? Lraw : L);
+                }
                 mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
                 for (int k = 0; k < DPL; k++) Lp[k] = L[k];

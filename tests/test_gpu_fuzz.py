@@ -279,3 +279,29 @@ def test_fuzz_host_batch_and_overlap_tiles(engine, oracle, synth, pkg, seed):
     bands = int(rng.integers(1, min(h, 4) + 1))
     got = engine.match_tiled(frames[0][0], frames[0][1], bands, h)
     assert np.array_equal(got, refs[0]), f"overlap tiles, {bands} bands, halo {h}, mode {mode} {h}x{w} {kw} {kind}"
+
+
+@pytest.mark.parametrize("seed", range(max(N_CASES // 4, 8)))
+def test_fuzz_ocv_large_disparity(engine, oracle, synth, pkg, seed):
+    """OpenCV modes with D > 512 (64-lane path lines, chunked one-pixel-per-wave WTA): random
+    windows up to the cfg's 2048, blocks, penalties, uniqueness and post filters."""
+    rng = np.random.default_rng(50_000 + seed)
+    mode = [pkg.MODE_OCV_SGBM5, pkg.MODE_OCV_HH8][seed % 2]
+    D = int(rng.choice([528, 640, 768, 1024, 1296, 1536, 2048]))
+    minD = int(rng.integers(-12, 13))
+    span = max(D + minD, 0)
+    h = int(rng.choice([1, 3, 7, 16, 23]))
+    w = span + int(rng.integers(1, 60)) if rng.random() < 0.9 else int(rng.integers(1, span + 4))
+    p1 = int(rng.integers(1, 300))
+    kw = dict(num_disparities=D, min_disparity=minD, p1=p1, p2=int(rng.integers(p1 + 1, 1200)),
+              block_size=int(rng.choice([1, 3, 5, 7, 9, 11, 15, 21])), prefilter_cap=int(rng.integers(1, 64)),
+              uniqueness_ratio=int(rng.choice([0, 1, 5, 10, 15, 30, 99, 100, 120])),
+              disp12_max_diff=int(rng.choice([-1, 0, 1, 2, 5])),
+              speckle_window_size=int(rng.choice([0, 0, 10, 50])), speckle_range=int(rng.integers(1, 4)))
+    kind = str(rng.choice(["pair", "pair", "noise", "flat"]))
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    left, right = _images(rng, synth, h, w, minD, min(D, 256), kind, seed)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"

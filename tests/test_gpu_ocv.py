@@ -202,11 +202,13 @@ def test_plugin_core_cpp_init_and_match(tmp_path, oracle, synth):
 
 @pytest.mark.parametrize("wide", ["", "1"], ids=["int16", "int32"])
 @pytest.mark.parametrize("mode,h,w,minD,D,block,spk", [(0, 20, 1400, 0, 1024, 5, 100), (1, 24, 1300, -7, 784, 3, 0),
-                                                       (0, 12, 2300, 3, 2048, 7, 0), (1, 28, 2200, 0, 1536, 5, 0)])
+                                                       (0, 12, 2300, 3, 2048, 7, 0), (1, 28, 2200, 0, 1536, 5, 0),
+                                                       (0, 16, 1340, -1, 1296, 3, 10), (1, 20, 1200, 0, 1040, 5, 0)])
 def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wide, mode, h, w, minD, D, block, spk):
     """D > 512 in the OpenCV modes (the node's cfg allows disparity ranges up to 2048):
-    64-lane path lines (16 or 32 values per lane) and the one-pixel-per-wave WTA in chunks of
-    1024 disparities, int16 and int32 (SGM_OCV_WIDE) volumes."""
+    64-lane path lines (16 or 32 values per lane; D % 32 = 16 above 1024 leaves one lane
+    straddling D, found by the D > 512 fuzz) and the one-pixel-per-wave WTA in chunks of 1024
+    disparities, int16 and int32 (SGM_OCV_WIDE) volumes."""
     if wide:
         monkeypatch.setenv("SGM_OCV_WIDE", wide)
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), min(D, 256), seed=D + h)
