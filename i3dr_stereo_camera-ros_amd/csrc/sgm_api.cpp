@@ -160,6 +160,10 @@ struct sgm_handle {
     // exact tile mode (sgm_match_tiled_exact): one handle per row band, each with a second
     // stream for its upward sweeps and four events (census, down, up, gather)
     std::vector<sgm_handle*> bands;
+    // OCV-mode frame batches: frames dealt over a few same-device handles, each with its own
+    // stream and workspace, so the small launches of one frame overlap another's
+    std::vector<sgm_handle*> par;
+    hipEvent_t par_ev = nullptr;   // recorded on the handle's stream, then each lane's done
     hipStream_t stream2 = nullptr;
     hipEvent_t bev[4] = {};
     // cross-call ordering: every call that uses the workspace records `done` on the stream it
@@ -685,6 +689,52 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     return ensure_ws(h, l.total);
 }
 
+// OCV-mode batch (sgm_match_device_batch on an OpenCV mode): frames dealt round-robin over
+// S same-device lanes (own stream + workspace each; SGM_OCV_STREAMS, default 4, 1 = one
+// frame after another on the handle's stream). Every lane starts after the work already on
+// h->stream, and h->stream waits for every lane, so the call keeps the single-stream contract.
+int ocv_batch_lanes(int n)
+{
+    const char* e = std::getenv("SGM_OCV_STREAMS");
+    const int s = e ? std::atoi(e) : 4;
+    return std::max(1, std::min({s, n, 8}));
+}
+
+int run_batch_ocv(sgm_handle* h, int W, int H, const uint8_t* const* dLs, const uint8_t* const* dRs, int n,
+                  size_t stride, int16_t* const* outs, size_t out_stride)
+{
+    const int S = ocv_batch_lanes(n);
+    while ((int)h->par.size() < S) h->par.push_back(nullptr);
+    if (!h->par_ev) HIP_TRY(hipEventCreateWithFlags(&h->par_ev, hipEventDisableTiming), "hipEventCreate");
+    std::vector<Geom> g(S);
+    std::vector<Layout> l(S);
+    for (int s = 0; s < S; s++) {
+        sgm_handle*& q = h->par[s];
+        if (!q) {
+            const int rc = sgm_create(&q, h->device);
+            if (rc) return fail(h, rc, "cannot open a batch lane");
+        }
+        q->params = h->params;
+        const int rc = prepare(q, W, H, false, g[s], l[s]);
+        if (rc) return fail(h, rc, q->err);
+    }
+    HIP_TRY(hipEventRecord(h->par_ev, h->stream), "hipEventRecord");
+    for (int s = 0; s < S; s++) HIP_TRY(hipStreamWaitEvent(h->par[s]->stream, h->par_ev, 0), "hipStreamWaitEvent");
+    for (int i = 0; i < n; i++) {
+        sgm_handle* q = h->par[i % S];
+        const int rc = run_pipeline(q, l[i % S], g[i % S], dLs[i], dRs[i], stride, outs[i], out_stride);
+        if (rc) return fail(h, rc, q->err);
+    }
+    for (int s = 0; s < S; s++) {
+        sgm_handle* q = h->par[s];
+        if (!q->done) HIP_TRY(hipEventCreateWithFlags(&q->done, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventRecord(q->done, q->stream), "hipEventRecord");
+        q->done_stream = q->stream;
+        HIP_TRY(hipStreamWaitEvent(h->stream, q->done, 0), "hipStreamWaitEvent");
+    }
+    return SGM_OK;
+}
+
 }  // namespace
 
 // ==================================================================================== C-ABI
@@ -732,7 +782,9 @@ void sgm_destroy(sgm_handle* h)
     if (!h) return;
     for (sgm_handle* s : h->sub) sgm_destroy(s);
     for (sgm_handle* s : h->bands) sgm_destroy(s);
+    for (sgm_handle* s : h->par) sgm_destroy(s);
     if (hipSetDevice(h->device) == hipSuccess) {
+        if (h->par_ev) (void)hipEventDestroy(h->par_ev);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (h->stream2) (void)hipStreamSynchronize(h->stream2);
         if (h->done_stream) (void)hipEventSynchronize(h->done);   // the last call on a caller's stream
@@ -836,6 +888,8 @@ int sgm_match_device_batch_rect(sgm_handle* h, const uint8_t* const* dLs, const 
     if (rc) {
     } else if (pipelined) {
         rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride, rectLs, rectRs, rect_stride);
+    } else if (h->params.mode != SGM_MODE_CENSUS8 && ocv_batch_lanes(n) > 1 && !h->profiling) {
+        rc = run_batch_ocv(h, W, H, dLs, dRs, n, stride, outs, out_stride);
     } else {
         for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
     }

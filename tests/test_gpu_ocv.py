@@ -230,3 +230,34 @@ def test_ocv_tall_boxes(engine, oracle, synth, pkg, block):
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("streams", ["3", "1", "8"])
+@pytest.mark.parametrize("mode,n", [(0, 5), (1, 4), (0, 2)])
+def test_ocv_device_batch_lanes(engine, oracle, synth, pkg, monkeypatch, streams, mode, n):
+    """sgm_match_device_batch in the OpenCV modes: frames dealt over same-device stream lanes
+    (SGM_OCV_STREAMS; 1 = one after another on the handle's stream) give each frame's own
+    result, with median + speckles, and the call stays ordered on the caller's stream."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("SGM_OCV_STREAMS", streams)
+    h, w = 60, 300
+    p = pkg.default_params(mode, min_disparity=3, num_disparities=48, block_size=5, speckle_window_size=20)
+    engine.set_params(p)
+    frames = [synth.stereo_pair(h, w, 3, 48, seed=700 + i) for i in range(n)]
+    dl = [torch.from_numpy(f[0]).cuda() for f in frames]
+    dr = [torch.from_numpy(f[1]).cuda() for f in frames]
+    out = torch.full((n, h, w), 777, dtype=torch.int16, device="cuda")
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    for _ in range(2):                    # twice: the lanes' workspaces are reused
+        out.fill_(777)
+        stream.wait_stream(torch.cuda.current_stream())
+        engine.match_device_batch([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], w, h, w,
+                                  [out[i].data_ptr() for i in range(n)], w, stream.cuda_stream)
+        with torch.cuda.stream(stream):
+            got = out.clone()                 # on the caller's stream: after every lane
+        stream.synchronize()
+        got = got.cpu().numpy()
+        op = to_oracle_params(oracle, p)
+        for i, (l, r, _) in enumerate(frames):
+            assert np.array_equal(got[i], oracle.match(op, l, r)), f"frame {i}"
