@@ -1001,9 +1001,8 @@ void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_b
                 __builtin_amdgcn_s_setprio(SGM_UPWTA_PRIO);   // the launch's longest blocks
 #endif
                 const UpWta uw{pick4(wf.vols, f), vol_bytes, pick4(wf.res, f)};
-                p16_rows<RC::DPL, EXACT, RC::LPL, true>(pick4(wf.cL, f), pick4(wf.cR, f), nullptr, nullptr, g, 1,
-                                                        pl.xb_lo[1] + (int)(it & 0x3FFFFFu) * RC::NL, pl, lds_dyn64,
-                                                        uw);
+                p16_rows<DPL, EXACT, 16, true>(pick4(wf.cL, f), pick4(wf.cR, f), nullptr, nullptr, g, 1,
+                                               pl.xb_lo[1] + (int)(it & 0x3FFFFFu) * 16, pl, lds_dyn64, uw);
             }
         } else {
             paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, it, lds_dyn64);
@@ -1082,7 +1081,7 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
     group = std::min(std::max(group, 1), kMaxGroup);
     up_group = std::min(std::max(up_group, 0), kMaxGroup);
     {
-        const int NL = rows_lines(g.D);
+        const int NL = 16;                 // up+WTA blocks: 16-lane lines (the WTA layout), 16 per block
         const int nb = (g.maxX1 - pl.xb_lo[1] + NL - 1) / NL;
         for (int b = 0; b < nb; b++)
             for (int f = 0; f < up_group; f++) v.push_back({4 * g.H + 4 * g.W, path_item(8, b, f)});
@@ -1221,7 +1220,7 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
 {
     const int n_census = ((g.W + 63) / 64) * ((g.H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
     dim3 grid(n_items + (up_wta ? 0 : g.H * wf.n) + n_census), block(kWG);
-    const size_t lds = std::max({up_wta ? upwta_lds_bytes<RowsCfg<DPL>::DPL>() : wta_lds_bytes<DPL>(g.W),
+    const size_t lds = std::max({up_wta ? upwta_lds_bytes<DPL>() : wta_lds_bytes<DPL>(g.W),
                                  sizeof(uint64_t) * rows_lds_codes<DPL>(), (size_t)(kCensusRows + 6) * 72});
     uint64_t* tr = trace_buffer((int)grid.x);
     // WTA rows interleaved one per 2.5 blocks (C3 sweeps, first build: after the paths 554
