@@ -38,3 +38,27 @@ for fn in files[-4:]:
         dur = s1[m] - s0[m]
         print(f"  {name:7s} waves {m.sum():6d} start {s0[m].min():7.0f}-{s0[m].max():7.0f} end max {s1[m].max():7.0f} "
               f"dur mean {dur.mean():7.1f} max {dur.max():7.1f}")
+
+# occupancy over time of the steady launch (second-to-last traced file is the k=ng-1 launch;
+# take the one with the most up+WTA waves and census blocks: a steady launch)
+best = None
+for fn in files:
+    a = np.fromfile(fn, np.uint64).reshape(-1, 4)
+    a = a[a[:, 3] > 0]
+    kind = (a[:, 0] >> np.uint64(62)).astype(int)
+    d = ((a[:, 0] & np.uint64(0xFFFFFFFF)).astype(np.int64) >> 24) & 0xFF
+    if ((kind == 0) & (d == 8)).sum() > 0 and (kind == 2).sum() > 0:
+        best = fn
+if best:
+    a = np.fromfile(best, np.uint64).reshape(-1, 4)
+    a = a[a[:, 3] > 0]
+    kind = (a[:, 0] >> np.uint64(62)).astype(int)
+    d = ((a[:, 0] & np.uint64(0xFFFFFFFF)).astype(np.int64) >> 24) & 0xFF
+    t0 = a[:, 2].astype(np.int64); t1 = a[:, 3].astype(np.int64)
+    T0 = t0.min(); s0 = (t0 - T0) / 100.0; s1 = (t1 - T0) / 100.0
+    span = s1.max()
+    print(f"== occupancy of {best} (span {span:.0f} us): active waves per 100 us [up+wta rows horiz census]")
+    for b in np.arange(0, span, 100):
+        act = (s0 < b + 100) & (s1 > b)
+        print(f"  {b:6.0f} {int((act & (kind == 0) & (d == 8)).sum()):5d} {int((act & (kind == 0) & (d < 6)).sum()):5d} "
+              f"{int((act & (kind == 0) & (d >= 6) & (d < 8)).sum()):5d} {int((act & (kind == 2)).sum()):5d}")
