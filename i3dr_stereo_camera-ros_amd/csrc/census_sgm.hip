@@ -27,6 +27,9 @@
 #define SGM_EXP 0          // timing-only experiments (results invalid): bit 0 row segments from row 0,
                            // bit 1 dir-1 volume stores to the trash slot, bit 2 WTA reads 7 volumes
 #endif
+#ifndef SGM_LRPRIO_HW
+#define SGM_LRPRIO_HW 37   // a horizontal-scan step in row-sweep steps, x/64
+#endif
 #ifndef SGM_UPWTA_PRIO
 #define SGM_UPWTA_PRIO 0   // s_setprio of the up+WTA blocks (0: default priority)
 #endif
@@ -317,7 +320,7 @@ __device__ __forceinline__ HChunk16 hload16(const uint64_t* cLr, const uint64_t*
     return c;
 }
 
-template <int DPL, bool EXACT, int DX>
+template <int DPL, bool EXACT, int DX, bool PRIO = false>
 __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                           uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
                                           int y0)
@@ -349,6 +352,7 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     HChunk16 cur = hload16<DPL, DX>(cLr, cRr, g, 0, p);
     HChunk16 nxt = cur;
     for (int b = 0; b * U < n; b++) {
+        if constexpr (PRIO) lr_prio(((n - b * U) * SGM_LRPRIO_HW) >> 6, g.H);   // a scan step ~0.58 row steps
         static_for<0, U>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
             if constexpr (t % 16 == 0) nxt = hload16<DPL, DX>(cLr, cRr, g, (b * U + t) / 16 + 1, p);
@@ -500,7 +504,7 @@ __host__ __device__ constexpr size_t upwta_lds_bytes() { return (size_t)8 * 2 * 
 
 // NL lines of direction dir starting at base column xb (DPL disparities per lane, LPL
 // lanes per line; lds: 2 * RowSeg<DPL, LPL>::BUF codes).
-template <int DPL, bool EXACT, int LPL, bool FUSE = false>
+template <int DPL, bool EXACT, int LPL, bool FUSE = false, bool PRIO = false>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
                                          int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{})
@@ -643,6 +647,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         __syncthreads();
     };
     for (int s = s0; s < s1; s += 4) {
+        if constexpr (PRIO) lr_prio(s1 - s, g.H);
         body(s, buf0, buf1, R1, R0);
         body(s + 1, buf1, buf0, R2, R1);
         body(s + 2, buf0, buf1, R3, R2);
@@ -655,7 +660,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 template <int DPL>
 __host__ __device__ constexpr int rows_lds_codes() { return 2 * RowSeg<RowsCfg<DPL>::DPL, RowsCfg<DPL>::LPL>::BUF; }
 
-template <int DPL, bool EXACT>
+template <int DPL, bool EXACT, bool PRIO = false>
 __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_bytes, size_t trash_off,
                                               const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
@@ -668,9 +673,9 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     const uint64_t* cR = pick4(pf.cR, f);
     uint8_t* V = pick4(pf.vols, f) + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
-    if (dir == 6) p16_horiz<DPL, EXACT, 1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-    else if (dir == 7) p16_horiz<DPL, EXACT, -1>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-    else p16_rows<RC::DPL, EXACT, RC::LPL>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
+    if (dir == 6) p16_horiz<DPL, EXACT, 1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else if (dir == 7) p16_horiz<DPL, EXACT, -1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
 }
 
 // SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
@@ -691,7 +696,7 @@ void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g,
 {
     __shared__ uint64_t lds[rows_lds_codes<DPL>()];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    paths_block16<DPL, EXACT>(pf, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
+    paths_block16<DPL, EXACT, true>(pf, vol_bytes, trash_off, g, pl, items[blockIdx.x], lds);
     if (trace && (threadIdx.x & 63) == 0)        // debug timeline (SGM_TRACE): one record per wave
         trace_record(trace, items[blockIdx.x], t0);
 }

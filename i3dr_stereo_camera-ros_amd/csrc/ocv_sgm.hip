@@ -25,6 +25,9 @@ constexpr int kMaxCost = 32767;
 #ifndef SGM_OCV_PF
 #define SGM_OCV_PF 8       // cost rows in flight per path line (D <= 64)
 #endif
+#ifndef SGM_OCV_PRIO
+#define SGM_OCV_PRIO 0     // longest-remaining-first wave priority (lr_prio) in k_ocv_paths
+#endif
 #ifndef SGM_OCV_PF_WIDE
 #define SGM_OCV_PF_WIDE 2  // the same for more disparities per lane (1080p D=128 MODE_SGBM paths:
                            // 1 step 1.42 ms, 2 steps 0.95, 3 steps 1.57, 4 steps 1.25)
@@ -588,7 +591,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             }
         };
         if (nmax > 0) steps(0, std::true_type{});
-        for (int i0 = PF; i0 < nmax; i0 += PF) steps(i0, std::false_type{});
+        for (int i0 = PF; i0 < nmax; i0 += PF) {
+            if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+            steps(i0, std::false_type{});
+        }
     } else {
         // larger volumes: 64-bit addresses, clamped to the line; steps past a line's end and
         // lanes past D store to a per-lane trash slot after the volumes (vols + trash_off)
@@ -623,7 +629,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             }
         };
         if (nmax > 0) steps(0, std::true_type{});
-        for (int i0 = PF; i0 < nmax; i0 += PF) steps(i0, std::false_type{});
+        for (int i0 = PF; i0 < nmax; i0 += PF) {
+            if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+            steps(i0, std::false_type{});
+        }
     }
 }
 

@@ -1,0 +1,11 @@
+# longest-remaining-first wave priority (SGM_LRPRIO): single-frame trace + interleaved A/B
+set -u
+mkdir -p gpurun_out/tr4
+for v in base lr; do
+  lib=i3dr_stereo_camera-ros_amd/lib/libsgm_hip.so
+  [ $v != base ] && lib=i3dr_stereo_camera-ros_amd/lib/variants/lib_$v.so
+  SGM_HIP_LIB=$lib TRACE_D=128 SGM_TRACE=gpurun_out/tr4/$v.%d timeout -k 10 200 python tools/dbg/trace_run.py > gpurun_out/tr4_$v.log 2>&1 || { tail gpurun_out/tr4_$v.log; exit 1; }
+  python tools/dbg/trace_analyze.py gpurun_out/tr4/$v.1
+done
+rm -rf gpurun_out/tr4
+LIBS=i3dr_stereo_camera-ros_amd/lib/libsgm_hip.so,i3dr_stereo_camera-ros_amd/lib/variants/lib_lr.so CASES=1080x1920x128,1080x1920x256 ROUNDS=2 timeout -k 10 300 python3 tools/dbg/lib_ab.py

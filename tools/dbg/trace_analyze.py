@@ -8,7 +8,7 @@ for path in sys.argv[1:]:
     T0 = t0.min()
     s0 = (t0 - T0) / 100.0  # us (100 MHz)
     s1 = (t1 - T0) / 100.0
-    dirs = (it >> 24).astype(int)
+    dirs = ((it & np.uint64(0xFFFFFFFF)) >> np.uint64(24)).astype(int)
     span = s1.max()
     hwi = hw.astype(np.int64)
     cu = (hwi & 0xFFFFFFFF) >> 8 & 0xF           # CU_ID bits 11:8

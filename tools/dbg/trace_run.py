@@ -7,9 +7,10 @@ from conftest import _load
 pkg = ge.load_package()
 synth = _load("sgm_synth", ge.PKG_DIR + "/synth.py")
 eng = pkg.Engine(0)
-left, right, _ = synth.stereo_pair(1080, 1920, 0, 256, seed=1)
-eng.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=256))
+D = int(os.environ.get("TRACE_D", "256"))
+left, right, _ = synth.stereo_pair(1080, 1920, 0, D, seed=1)
+eng.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D))
 out = os.environ["SGM_TRACE"]
 for rep in range(3):
     eng.match(left, right)
-print("ok", os.path.getsize(out))
+print("ok")
