@@ -12,10 +12,11 @@
 //   k_ocv_paths      each direction independently (L depends only on its own path), four
 //                    lines per wave (16 lanes each);
 //                    int16 storage of L and minL as OpenCV's CostType
-//   k_ocv_wta16      S = saturate(sum of L) (all L >= 0 inside the parity domain, so the
-//                    saturating order is irrelevant), 16 lanes per pixel, + the shared
-//                    disp2 / LR row code.
-// Parity domain: SAD + 2*P2 <= 32767 (always true for block <= 15 at the node defaults).
+//   k_ocv_wta16      S = the sum of L in OpenCV's saturating order, 16 lanes per pixel, + the
+//                    shared disp2 / LR row code (k_ocv_wta64 for D > 512).
+// Volumes: int16 while no path cost can leave int16; otherwise (Geom::wide, e.g. the shipped
+// 2448x2048 D=480 block-21 config) int32 path volumes, gated per frame by the cost kernel's
+// overflow flag ("OpenCV semantics targets").
 #include "sgm_device.h"
 #include <cstdlib>
 
@@ -109,158 +110,201 @@ __global__ __launch_bounds__(256) void k_ocv_hsum(const int16_t* __restrict__ pi
 // output columns (few halo columns recomputed) at any D: with all D in one block it could
 // take only 32 columns, and a 21-wide box recomputed 52 columns per 32 outputs (the shipped
 // 2448x2048 D=480 block-21 config: 5.38 -> 3.38 ms).
+// Every value is handled as a packed pair of ADJACENT DISPARITIES (d, d+1) in one u32, the
+// layout of the output volume, so the box and its stores take one op per two cells:
 //   stage:  the Birchfield-Tomasi intervals (u, lo, hi) of both channels of the NX = XB + 2*SW2
-//           left columns and of the NR = NX + DC - 1 right columns they meet, as u16 planes
-//           (the right ones twice, the second copy shifted by one, so a 32-bit read at either
-//           parity returns two adjacent entries);
-//   cost:   P[d][k] for column pairs (k, k+1): the pair's left and right entries are adjacent
-//           (r = k + DC - 1 - d), so one u32 read per plane and packed i16 arithmetic give two
-//           cells (≈10 packed ops and 3 LDS reads per cell, was ≈33 VALU and 13 LDS);
-//   box:    thread (segment, d) slides its window over the segment's outputs, 2 LDS reads per
-//           output; columns outside [0, width1) read the edge column (the running sum's
-//           replicate rule).
-constexpr int kPixXB = 128;     // output columns per block
-constexpr int kPixDC = 128;     // disparities per block
+//           left columns, each duplicated into both halves of a u32, 6 words per column; the
+//           right entries the cells reach (r = 0 .. NX + DC - 2), indexed j = M - 1 - r, as pair
+//           words W[j] = (entry j, entry j + 1) per plane: the right entries of (d, d+1) at one
+//           column are W[j] of d (low = d, high = d + 1). Records of 6 words (+ 1 pad) per j,
+//           even and odd j apart: the lanes of a wave read j, j + 2, ... at a stride of 7 words
+//           (conflict-free), the planes at immediate offsets;
+//   cost:   P[k][dp] = the cells (k, 2dp) and (k, 2dp + 1): 12 u32 reads at immediate offsets
+//           from two running addresses, packed u16 saturating subtracts (max(a - b, 0) in one
+//           op): 16 packed ops for two cells;
+//   edges:  staged columns outside [0, width1) take the edge column's P (the running sum's
+//           replicate rule), in a short pass that only edge blocks run;
+//   box:    thread (segment, dp) slides its window over the segment's outputs: two u32 LDS
+//           reads, one packed subtract and add, one u32 store per two cells (u16 wrap-around
+//           = OpenCV's int16 truncation of the int sum).
+#ifndef SGM_PIX_XB
+#define SGM_PIX_XB 128
+#endif
+#ifndef SGM_PIX_DC
+#define SGM_PIX_DC 128
+#endif
+constexpr int kPixXB = SGM_PIX_XB;     // output columns per block
+constexpr int kPixDC = SGM_PIX_DC;     // disparities per block
 __host__ __device__ inline int pix_xb(const Geom& g) { return g.D >= kPixDC ? kPixXB : kPixXB * 2; }
 __host__ __device__ inline int pix_dc(const Geom& g) { return g.D < kPixDC ? g.D : kPixDC; }
 struct PixGeo {
-    int XB, DC, NX, NR, NXP;    // NX even; NXP: P's row pitch in u16, NXP/2 odd (conflict-free columns)
+    int XB, DC, NX, M, PP;      // NX even >= XB + 2*SW2; M: right pair words (j < M);
+                                // PP: P's row pitch in u32 (odd below 64 pairs: rows spread over banks)
     __host__ __device__ PixGeo(const Geom& g) {
         XB = pix_xb(g); DC = pix_dc(g);
         NX = (XB + 2 * g.SW2 + 1) & ~1;
-        NR = (NX + DC) & ~1;                        // >= NX + DC - 1 entries, even
-        NXP = (NX / 2) % 2 ? NX : NX + 2;
+        M = ((NX + DC) & ~1) + 2;                   // even, > NX + DC - 1; M / 2 records per parity
+        PP = DC / 2 >= 64 ? DC / 2 : DC / 2 + 1;
     }
-    __host__ __device__ size_t bytes() const { return (size_t)2 * ((size_t)DC * NXP + 6 * NX + 12 * (NR + 2)); }
+    __host__ __device__ size_t bytes() const { return (size_t)4 * ((size_t)NX * PP + 6 * NX + 7 * M); }
 };
 __host__ inline size_t pix_lds_bytes(const Geom& g) { return PixGeo(g).bytes(); }
-typedef short s16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__ planes, Geom g,
                                                      int16_t* __restrict__ hs)
 {
     extern __shared__ uint32_t lds_pix32[];
     const PixGeo pg(g);
-    const int XB = pg.XB, DCmax = pg.DC, NX = pg.NX, NR = pg.NR, NXP = pg.NXP;
+    const int XB = pg.XB, DCmax = pg.DC, NX = pg.NX, M = pg.M, PP = pg.PP;
     const int y = blockIdx.y, x0 = blockIdx.x * XB, tid = threadIdx.x;
-    const int d0 = blockIdx.z * DCmax, DC = min(DCmax, g.D - d0);
+    const int d0 = blockIdx.z * DCmax, DC = min(DCmax, g.D - d0), DPC = DC / 2;   // D % 16 == 0: DC even
     const int SW2 = g.SW2;
     const size_t plane = (size_t)g.W * g.H;
-    uint16_t* P = (uint16_t*)lds_pix32;                    // [DCmax][NXP]
-    uint16_t* Lp = P + (size_t)DCmax * NXP;                // 6 planes x NX: (u, lo, hi) of channel 0, then 1
-    uint16_t* Rp = Lp + 6 * NX;                            // 6 planes x (NR + 2)
-    uint16_t* Rs = Rp + 6 * (NR + 2);                      // the same shifted by one entry
+    uint32_t* P = lds_pix32;                               // [NX][PP] packed (d, d+1)
+    uint32_t* Lx = P + (size_t)NX * PP;                    // [NX][6]: (u, lo, hi) of channel 0, then 1
+    uint32_t* Rw = Lx + 6 * NX;                            // [j & 1][j >> 1][7] pair words, same plane order
+    const int MH = M / 2;
     // staged column k <-> x = minX1 + x0 - SW2 + k (not clamped: out-of-frame columns get
-    // clamped BT entries and are never summed); right entry r <-> xr = x(0) - minD - (d0 + DC - 1) + r
+    // clamped BT entries and are replaced by the edge pass); right entry r <-> xr = x(0) - minD - (d0 + DC - 1) + r
     const int xs = g.minX1 + x0 - SW2;
     for (int i = tid; i < 2 * NX; i += 256) {
         const int c = i / NX, k = i - c * NX;
         int u, lo, hi;
         bt_lohi(planes + c * plane + (size_t)y * g.W, min(max(xs + k, 0), g.W - 1), g.W, u, lo, hi);
-        Lp[(3 * c) * NX + k] = (uint16_t)u; Lp[(3 * c + 1) * NX + k] = (uint16_t)lo; Lp[(3 * c + 2) * NX + k] = (uint16_t)hi;
+        uint32_t* o = Lx + 6 * k + 3 * c;
+        o[0] = (uint32_t)u * 0x10001u; o[1] = (uint32_t)lo * 0x10001u; o[2] = (uint32_t)hi * 0x10001u;
     }
     const int xr0 = xs - g.minD - (d0 + DC - 1);
-    for (int i = tid; i < 2 * (NR + 1); i += 256) {
-        const int c = i / (NR + 1), r = i - c * (NR + 1);
+    const int NRr = NX + DC - 1;                           // right entries the cells reach
+    uint16_t* Rh = (uint16_t*)Rw;
+    for (int i = tid; i < 2 * NRr; i += 256) {
+        const int c = i / NRr, r = i - c * NRr;
         int v, lo, hi;
         bt_lohi(planes + (2 + c) * plane + (size_t)y * g.W, min(max(xr0 + r, 0), g.W - 1), g.W, v, lo, hi);
-        const int q = 3 * c * (NR + 2);
-        Rp[q + r] = (uint16_t)v; Rp[q + (NR + 2) + r] = (uint16_t)lo; Rp[q + 2 * (NR + 2) + r] = (uint16_t)hi;
-        if (r > 0) { Rs[q + r - 1] = (uint16_t)v; Rs[q + (NR + 2) + r - 1] = (uint16_t)lo; Rs[q + 2 * (NR + 2) + r - 1] = (uint16_t)hi; }
+        // entry j = M - 1 - r: low half of word j, high half of word j - 1 (j >= 2)
+        const int j = M - 1 - r;
+        uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
+        uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
+        lo16[0] = (uint16_t)v; lo16[2] = (uint16_t)lo; lo16[4] = (uint16_t)hi;
+        hi16[0] = (uint16_t)v; hi16[2] = (uint16_t)lo; hi16[4] = (uint16_t)hi;
     }
     __syncthreads();
-    // thread -> disparity d (fixed), column pairs kp, kp + step, ...
-    const int npair = NX / 2, tpd = 256 / DCmax;           // threads per disparity
-    const int d = tid % DCmax, kp0 = tid / DCmax;
-    if (d < DC && kp0 < tpd) {
-        const int roff = DC - 1 - d;                       // r = k + roff
-        const uint16_t* R = (roff & 1) ? Rs + (roff - 1) : Rp + roff;   // u32-aligned for every even k
-        auto rd = [&](const uint16_t* base, int off) { return __builtin_bit_cast(s16x2_t, *(const uint32_t*)(base + off)); };
-        const s16x2_t zero = {0, 0};
-        for (int kp = kp0; kp < npair; kp += tpd) {
-            const int k = 2 * kp;
-            s16x2_t acc = zero;
+    // thread -> disparity pair dp (fixed), columns k = kg, kg + tpd, ...
+    // cell (k, d): r = k + DC - 1 - d, j = M - 1 - r = M - DC - k + d; the pair (2dp, 2dp + 1)
+    // reads word j of d = 2dp (entries j and j + 1 = the right entries of d and d + 1). tpd is
+    // even, so a thread's j keeps its parity (j = k mod 2) and steps tpd / 2 records down.
+    const int tpd = (256 / DPC) & ~1, dp = tid % DPC, kg = tid / DPC;
+    if (kg < tpd) {
+        auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
+        auto w = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
+        const uint32_t* Lk = Lx + 6 * kg;
+        const int j0 = M - DC - kg + 2 * dp;
+        const uint32_t* Rk = Rw + 7 * ((j0 & 1) * MH + (j0 >> 1));
+        uint32_t* Pk = P + (size_t)kg * PP + dp;
+        for (int k = kg; k < NX; k += tpd, Lk += 6 * tpd, Rk -= 7 * (tpd / 2), Pk += tpd * PP) {
+            u16x2_t m[2];
 #pragma unroll
             for (int c = 0; c < 2; c++) {
-                const s16x2_t u = rd(Lp, (3 * c) * NX + k), ulo = rd(Lp, (3 * c + 1) * NX + k), uhi = rd(Lp, (3 * c + 2) * NX + k);
-                const int q = 3 * c * (NR + 2);
-                const s16x2_t v = rd(R, q + k), v0 = rd(R, q + (NR + 2) + k), v1 = rd(R, q + 2 * (NR + 2) + k);
-                const s16x2_t c0 = __builtin_elementwise_max(__builtin_elementwise_max(u - v1, v0 - u), zero);
-                const s16x2_t c1 = __builtin_elementwise_max(__builtin_elementwise_max(v - uhi, ulo - v), zero);
-                const s16x2_t m = __builtin_elementwise_min(c0, c1);
-                acc += c == 0 ? m : (m >> (s16x2_t){2, 2});
+                const u16x2_t u = w(Lk, 3 * c), ulo = w(Lk, 3 * c + 1), uhi = w(Lk, 3 * c + 2);
+                const u16x2_t v = w(Rk, 3 * c), v0 = w(Rk, 3 * c + 1), v1 = w(Rk, 3 * c + 2);
+                const u16x2_t c0 = __builtin_elementwise_max(sat(u, v1), sat(v0, u));
+                const u16x2_t c1 = __builtin_elementwise_max(sat(v, uhi), sat(ulo, v));
+                m[c] = __builtin_elementwise_min(c0, c1);
             }
-            *(uint32_t*)(P + (size_t)d * NXP + k) = __builtin_bit_cast(uint32_t, acc);
+            *Pk = __builtin_bit_cast(uint32_t, m[0] + (m[1] >> (u16x2_t){2, 2}));
         }
     }
     __syncthreads();
-    // horizontal box: thread (segment, d) slides its window over the segment's outputs
     const int nout = min(XB, g.width1 - x0);
     const int klo = SW2 - x0, khi = g.width1 - 1 - x0 + SW2;   // staged columns inside [0, width1)
-    auto pk = [&](const uint16_t* Pd, int k) { return (int)(int16_t)Pd[min(max(k, klo), khi)]; };
+    if (klo > 0 || khi < NX - 1) {                              // uniform: an edge block
+        const int nlo = max(klo, 0), nhi = max(NX - 1 - khi, 0);
+        for (int i = tid; i < (nlo + nhi) * DPC; i += 256) {
+            const int e = i / DPC, p = i - e * DPC;
+            const int k = e < nlo ? e : khi + 1 + (e - nlo);
+            P[(size_t)k * PP + p] = P[(size_t)(e < nlo ? klo : khi) * PP + p];
+        }
+        __syncthreads();
+    }
+    // horizontal box: thread (segment, dp) slides its window over the segment's outputs
     int16_t* dst = hs + ((size_t)y * g.width1 + x0) * g.D + d0;
-    const int nseg = max(256 / DC, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
-    for (int t = tid; t < nseg * DC; t += 256) {
-        const int seg = t / DC, dd = t - seg * DC;
+    const int nseg = max(256 / DPC, 1), seglen = (nout + nseg - 1) / nseg, BW = 2 * SW2;
+    for (int t = tid; t < nseg * DPC; t += 256) {
+        const int seg = t / DPC, p = t - seg * DPC;
         const int xa = seg * seglen, xb = min(xa + seglen, nout);
         if (xa >= xb) continue;
-        const uint16_t* Pd = P + (size_t)dd * NXP;
-        int sum = 0;
-        for (int u = 0; u <= BW; u++) sum += pk(Pd, xa + u);
-        dst[(size_t)xa * g.D + dd] = (int16_t)sum;
+        const uint32_t* Pd = P + p;
+        u16x2_t sum = {0, 0};
+        for (int u = 0; u <= BW; u++) sum += __builtin_bit_cast(u16x2_t, Pd[(size_t)(xa + u) * PP]);
+        uint32_t* o = (uint32_t*)(dst + (size_t)xa * g.D) + p;
+        *o = __builtin_bit_cast(uint32_t, sum);
         for (int xo = xa + 1; xo < xb; xo++) {
-            sum += pk(Pd, xo + BW) - pk(Pd, xo - 1);
-            dst[(size_t)xo * g.D + dd] = (int16_t)sum;
+            sum += __builtin_bit_cast(u16x2_t, Pd[(size_t)(xo + BW) * PP]) - __builtin_bit_cast(u16x2_t, Pd[(size_t)(xo - 1) * PP]);
+            o += g.D / 2;
+            *o = __builtin_bit_cast(uint32_t, sum);
         }
     }
 }
 
 // Vertical box + P2 offset + the bottom-row rule, in segments of kVsumRows rows per thread
 // (each segment starts from its own window sum; rows y >= 1 with y + SH2 >= H repeat the
-// value of row max(H - SH2 - 1, 0) in MODE_SGBM, or are P2 in MODE_HH).
-constexpr int kVsumRows = 64;
+// value of row max(H - SH2 - 1, 0) in MODE_SGBM, or are P2 in MODE_HH). A thread owns two
+// adjacent disparities (one u32 of the row: width1 * D is even), int sums per half (the
+// overflow flag needs the true value), one u32 load per row and window edge, one u32 store.
+#ifndef SGM_VSUM_ROWS
+#define SGM_VSUM_ROWS 64
+#endif
+constexpr int kVsumRows = SGM_VSUM_ROWS;
 __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict__ hs, Geom g, int fullDP,
                                                       int16_t* __restrict__ C)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= g.width1 * g.D) return;
-    const size_t rs = (size_t)g.width1 * g.D;
+    const int i = blockIdx.x * 256 + threadIdx.x;         // pair index in a row
+    const size_t rs = (size_t)g.width1 * g.D / 2;          // u32 per row
+    if (i >= (int)rs) return;
+    const uint32_t* h32 = (const uint32_t*)hs;
+    uint32_t* C32 = (uint32_t*)C;
     const int H = g.H, SH2 = g.SH2;
     const int y0 = blockIdx.y * kVsumRows, y1 = min(H, y0 + kVsumRows);
-    auto window = [&](int y) {
-        int s = 0;
-        for (int k = y - SH2; k <= y + SH2; k++) s += hs[(size_t)min(max(k, 0), H - 1) * rs + i];
-        return s;
+    auto lo16 = [](uint32_t w) { return (int)(int16_t)(uint16_t)w; };
+    auto hi16 = [](uint32_t w) { return (int)w >> 16; };
+    auto window = [&](int y, int& s0, int& s1) {
+        s0 = 0; s1 = 0;
+        for (int k = y - SH2; k <= y + SH2; k++) {
+            const uint32_t w = h32[(size_t)min(max(k, 0), H - 1) * rs + i];
+            s0 += lo16(w); s1 += hi16(w);
+        }
     };
     bool ovf = false;                                      // a C' above int16 (Geom::wide == 2)
     const int ylast = max(H - SH2 - 1, 0);                 // last row whose window is recomputed
     const bool tail = y1 - 1 >= 1 && y1 - 1 + SH2 >= H;    // the segment reaches the repeated rows
-    const int rep = fullDP ? g.P2 : g.P2 + (tail ? window(ylast) : 0);
-    int s = window(y0);
+    int rep0 = g.P2, rep1 = g.P2;
+    if (!fullDP && tail) { int t0, t1; window(ylast, t0, t1); rep0 += t0; rep1 += t1; }
+    int s0, s1;
+    window(y0, s0, s1);
     // rows in chunks of 8: the chunk's 16 entering / leaving rows are loaded together (clamped
-    // rows, used only where the window slides), so a thread keeps 16 loads in flight instead
-    // of one dependent pair per row (C1: 30 -> 24 us)
+    // rows, used only where the window slides), so a thread keeps 16 loads in flight
     constexpr int U = 8;
     for (int yb = y0; yb < y1; yb += U) {
-        int ha[U], hb[U];
+        uint32_t ha[U], hb[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int y = min(yb + u, y1 - 1);
-            ha[u] = hs[(size_t)min(y + SH2, H - 1) * rs + i];
-            hb[u] = hs[(size_t)max(y - SH2 - 1, 0) * rs + i];
+            ha[u] = h32[(size_t)min(y + SH2, H - 1) * rs + i];
+            hb[u] = h32[(size_t)max(y - SH2 - 1, 0) * rs + i];
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int y = yb + u;
             if (y >= y1) break;                            // uniform over the block
-            int v;
+            int v0, v1;
             if (y == 0 || y + SH2 < H) {
-                if (y > y0) s += ha[u] - hb[u];
-                v = g.P2 + s;
+                if (y > y0) { s0 += lo16(ha[u]) - lo16(hb[u]); s1 += hi16(ha[u]) - hi16(hb[u]); }
+                v0 = g.P2 + s0; v1 = g.P2 + s1;
             } else {
-                v = rep;
+                v0 = rep0; v1 = rep1;
             }
-            ovf |= v > kMaxCost;
-            C[(size_t)y * rs + i] = (int16_t)v;
+            ovf |= max(v0, v1) > kMaxCost;
+            C32[(size_t)y * rs + i] = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
         }
     }
     if (g.wide == 2 && g.ovf) {                            // one atomic per wave that saw one
@@ -809,7 +853,7 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
         hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
         hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
     }
-    hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows), dim3(256),
+    hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D / 2 + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows), dim3(256),
                        0, st, bufB, g, fullDP, bufA);
     return hipGetLastError();
 }
