@@ -532,6 +532,9 @@ __device__ __forceinline__ int line_min_i32(int v)
     return v;
 }
 
+// buffer offset of a dropped store: past every buffer range the buffer path is used for
+constexpr uint32_t kBufDrop = 0xFFFFFF00u;
+
 // 64 / LPL path lines per wave. Block b of direction dir holds its lines NLW*b .. NLW*b +
 // NLW - 1: horizontal (ry == 0) line = row; row sweeps (ry != 0): lines [0, width1) start on
 // the first row at that column, the others on the entry column at row offset
@@ -598,15 +601,15 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop).
     // The first PF steps are peeled (pv = false only at step 0, a constant elsewhere).
     if (use_buf) {
-        // Volumes < 2 GB: raw buffer loads and stores with 32-bit byte offsets that just move
-        // by the step; a step past the line's end reads whatever lies there (unused) or 0 past
-        // the range, and a store that must not land is sent past the range, where the hardware
-        // drops it. No clamps, 64-bit address selects or trash slot in the step chain (C1
+        // Volumes < 4 GB - 256 B: raw buffer loads and stores with 32-bit byte offsets that just
+        // move by the step (mod 2^32); a step past the line's end reads whatever lies there
+        // (unused) or 0 past the range, and a store that must not land is sent to kBufDrop,
+        // past the range, where the hardware drops it. No clamps, 64-bit address selects or trash slot in the step chain (C1
         // paths 115 -> 90 us: a small frame's line is issue-bound, 61 -> 48 instructions/step).
         const size_t cells = (size_t)g.width1 * g.H * g.D;
-        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(cells * 2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(uint32_t)(cells * 2), 0x00020000);
         const __amdgpu_buffer_rsrc_t rsV =
-            __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)(cells * sizeof(VT)), 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)(uint32_t)(cells * sizeof(VT)), 0x00020000);
         const uint32_t bstep = (uint32_t)(cstep * 2), vstep = (uint32_t)(cstep * (long long)sizeof(VT));
         uint32_t ld_b = (uint32_t)((cbase + dl) * 2), st_b = (uint32_t)((cbase + dl) * (long long)sizeof(VT));
 #pragma unroll
@@ -620,11 +623,11 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                 const bool ok = lane_act && i < n;
                 if constexpr (DPL == 32) {        // two halves: the straddling lane drops its upper one
                     const int (&Vs)[32] = kRaw ? Lraw : L;
-                    bstore_vals<VT, 16>(rsV, ok ? st_b : 0x80000000u, *reinterpret_cast<const int(*)[16]>(&Vs[0]));
-                    bstore_vals<VT, 16>(rsV, ok && !straddle ? st_b + 16u * (uint32_t)sizeof(VT) : 0x80000000u,
+                    bstore_vals<VT, 16>(rsV, ok ? st_b : kBufDrop, *reinterpret_cast<const int(*)[16]>(&Vs[0]));
+                    bstore_vals<VT, 16>(rsV, ok && !straddle ? st_b + 16u * (uint32_t)sizeof(VT) : kBufDrop,
                                         *reinterpret_cast<const int(*)[16]>(&Vs[16]));
                 } else {
-                    bstore_vals<VT, DPL>(rsV, ok ? st_b : 0x80000000u, kRaw ? Lraw : L);
+                    bstore_vals<VT, DPL>(rsV, ok ? st_b : kBufDrop, kRaw ? Lraw : L);
                 }
                 mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
 #pragma unroll
@@ -877,8 +880,9 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
         total += nb[i];
     }
     const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
-    // 32-bit buffer offsets when a volume is < 2 GB (SGM_OCV_NO_BUF=1 forces the 64-bit path)
-    const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < 0x7FFFFFFFu && !getenv("SGM_OCV_NO_BUF");
+    // 32-bit buffer offsets when a volume ends below kBufDrop (the shipped 2448x2048 D=480
+    // config's int16 volumes are 3.6 GB; SGM_OCV_NO_BUF=1 forces the 64-bit path)
+    const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < (size_t)kBufDrop && !getenv("SGM_OCV_NO_BUF");
     hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf);
 }

@@ -68,8 +68,9 @@ def test_reference_config_gate_takes_int32_on_overflow(engine, oracle, pkg, mode
 @pytest.mark.parametrize("mode", ["sgbm", "hh"])
 def test_reference_config_full_frame_properties(engine, pkg, ref_frame, mode, monkeypatch):
     """The whole 2448 x 2048 frame (the CPU oracle takes minutes at this size): repeatable,
-    identical through the gated int16 and the forced int32 volumes, inside the search window
-    and close to the synthetic truth."""
+    identical through the gated int16 volumes (3.6 GB each: the 32-bit buffer-offset path
+    kernel), the same with 64-bit addresses (SGM_OCV_NO_BUF=1) and the forced int32 volumes,
+    inside the search window and close to the synthetic truth."""
     left, right, truth = ref_frame
     p = _params(pkg, mode)
     engine.set_params(p)
@@ -79,6 +80,10 @@ def test_reference_config_full_frame_properties(engine, pkg, ref_frame, mode, mo
     monkeypatch.setenv("SGM_OCV_GATE", "0")
     c = engine.match(left, right)
     assert np.array_equal(a, c), f"gated vs int32 volumes: {(a != c).sum()} pixels differ"
+    monkeypatch.delenv("SGM_OCV_GATE")
+    monkeypatch.setenv("SGM_OCV_NO_BUF", "1")
+    d = engine.match(left, right)
+    assert np.array_equal(a, d), f"buffer offsets vs 64-bit addresses: {(a != d).sum()} pixels differ"
     valid = a != (147 - 1) * 16
     assert valid.mean() > 0.5
     err = np.abs(a[valid] / 16.0 - truth[valid])
