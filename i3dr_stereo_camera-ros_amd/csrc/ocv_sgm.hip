@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void k_ocv_hsum(const int16_t* __restrict__ pi
 #ifndef SGM_PIX_DC
 #define SGM_PIX_DC 128
 #endif
-constexpr int kPixXB = SGM_PIX_XB;     // output columns per block (32/64/96/128 measured: 96 best at the shipped config)
+constexpr int kPixXB = SGM_PIX_XB;     // output columns per block (32-128 measured: 96 best at the shipped config)
 constexpr int kPixDC = SGM_PIX_DC;     // disparities per block
 __host__ __device__ inline int pix_xb(const Geom& g) { return g.D >= kPixDC ? kPixXB : kPixXB * 2; }
 __host__ __device__ inline int pix_dc(const Geom& g) { return g.D < kPixDC ? g.D : kPixDC; }
