@@ -36,6 +36,23 @@ HIP_StereoSGM = 6
 
 MISSING_Z = 10000.0  # image_geometry::StereoCameraModel::MISSING_Z
 
+# sgm_params.ocv_compat: the OpenCV build the OCV modes reproduce (include/sgm_hip.h SGM_OCV_*)
+OCV_COL0_LEGACY, OCV_SIMD_SAT, OCV_LANE_TIE = 1, 2, 4
+COMPAT_SCALAR = 0                                               # scalar 4.x restatement
+COMPAT_NOETIC = OCV_SIMD_SAT                                    # noetic x86-64 (OpenCV 4.2)
+COMPAT_MELODIC = OCV_COL0_LEGACY | OCV_SIMD_SAT | OCV_LANE_TIE  # melodic x86-64 (OpenCV 3.2), default
+COMPAT_NAMES = {"scalar": COMPAT_SCALAR, "noetic": COMPAT_NOETIC, "melodic": COMPAT_MELODIC}
+
+
+def ocv_compat_from_env(default=COMPAT_MELODIC):
+    """SGM_HIP_OCV_COMPAT = melodic | noetic | scalar | <bits> (the adapters read the same
+    variable)."""
+    v = os.environ.get("SGM_HIP_OCV_COMPAT")
+    if not v:
+        return default
+    v = v.strip().lower()
+    return COMPAT_NAMES[v] if v in COMPAT_NAMES else int(v, 0) & 7
+
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
     "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
@@ -52,7 +69,7 @@ class SgmParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "mode", "min_disparity", "num_disparities", "block_size", "p1", "p2",
         "uniqueness_ratio", "disp12_max_diff", "prefilter_cap", "speckle_window_size",
-        "speckle_range", "subpixel", "lr_check", "median")]
+        "speckle_range", "subpixel", "lr_check", "median", "ocv_compat")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -265,8 +282,11 @@ class Engine:
         h, w = lefts[0].shape
 
         def rows(arrs, dtype):
+            # a row-strided view passes as is; broadcast / overlapping / reversed views
+            # (strides[0] < w * itemsize or <= 0) are compacted first
             arrs = [a if (a.dtype == dtype and a.ndim == 2 and a.strides[1] == a.itemsize and
-                          a.strides[0] % a.itemsize == 0) else np.ascontiguousarray(a, dtype) for a in arrs]
+                          a.strides[0] % a.itemsize == 0 and a.strides[0] >= w * a.itemsize)
+                    else np.ascontiguousarray(a, dtype) for a in arrs]
             st = {a.strides[0] // a.itemsize for a in arrs}
             if len(st) != 1:   # one stride per side: compact the odd ones out
                 arrs = [np.ascontiguousarray(a) for a in arrs]
@@ -552,6 +572,7 @@ class MatcherHIPSGM:
     def init(self):
         # cv::StereoSGBM::create(64, 9, 5) equivalent starting point (matcherOpenCVSGBM.cpp:14)
         p = default_params(self.mode)
+        p.ocv_compat = ocv_compat_from_env(p.ocv_compat)
         p.min_disparity, p.num_disparities, p.block_size = 64, 9, 5
         p.p1 = p.p2 = p.uniqueness_ratio = p.disp12_max_diff = p.prefilter_cap = 0
         p.speckle_window_size = p.speckle_range = 0

@@ -11,6 +11,9 @@
 // stored); S never touches HBM.
 #include "sgm_device.h"
 
+#include <atomic>
+#include <string>
+
 #ifndef SGM_WPE
 #define SGM_WPE 4          // minimum waves per SIMD of the path kernels (register budget)
 #endif
@@ -26,6 +29,9 @@
 #ifndef SGM_EXP
 #define SGM_EXP 0          // timing-only experiments (results invalid): bit 0 row segments from row 0,
                            // bit 1 dir-1 volume stores to the trash slot, bit 2 WTA reads 7 volumes
+#endif
+#if SGM_EXP != 0 && !defined(SGM_EXPERIMENT_BUILD)
+#error "SGM_EXP builds give invalid results: define SGM_EXPERIMENT_BUILD as well (never in a release build)"
 #endif
 #ifndef SGM_LRPRIO_HW
 #define SGM_LRPRIO_HW 37   // a horizontal-scan step in row-sweep steps, x/64
@@ -1147,11 +1153,15 @@ static void trace_dump(uint64_t* tr, int n_blocks, hipStream_t st)
     std::vector<uint64_t> h((size_t)n_blocks * 16);
     if (hipStreamSynchronize(st) == hipSuccess &&
         hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-        // a '%d' in the name numbers the dumps (one file per traced launch)
-        static int n_dump = 0;
-        char name[512];
-        snprintf(name, sizeof name, getenv("SGM_TRACE"), n_dump++);
-        FILE* f = fopen(name, "wb");
+        // the first '%d' in the name is replaced by the dump number (one file per traced
+        // launch); the value is never used as a format string
+        static std::atomic<int> n_dump{0};
+        const std::string pat = getenv("SGM_TRACE");
+        const size_t at = pat.find("%d");
+        const std::string name = at == std::string::npos
+                                     ? pat
+                                     : pat.substr(0, at) + std::to_string(n_dump++) + pat.substr(at + 2);
+        FILE* f = fopen(name.c_str(), "wb");
         if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
     }
 }

@@ -18,6 +18,7 @@
 // 2448x2048 D=480 block-21 config) int32 path volumes, gated per frame by the cost kernel's
 // overflow flag ("OpenCV semantics targets").
 #include "sgm_device.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace sgm {
@@ -63,11 +64,11 @@ __device__ __forceinline__ void bt_lohi(const uint8_t* a, int x, int W, int& u, 
     hi = max(max(ul, ur), u);
 }
 
-// grid (width1, H), block 256 over d
-__global__ __launch_bounds__(256) void k_ocv_pixcost(const uint8_t* __restrict__ planes, Geom g,
-                                                     int16_t* __restrict__ cost)
+__device__ __forceinline__ int sat16(int v) { return min(max(v, -32768), 32767); }
+
+__device__ __forceinline__ void pixcost_cell(const uint8_t* __restrict__ planes, const Geom& g, int x1, int y,
+                                             int16_t* __restrict__ cost)
 {
-    const int x1 = blockIdx.x, y = blockIdx.y;
     const int x = x1 + g.minX1;
     const size_t plane = (size_t)g.W * g.H;
     int c_u[2], c_lo[2], c_hi[2];
@@ -87,6 +88,13 @@ __global__ __launch_bounds__(256) void k_ocv_pixcost(const uint8_t* __restrict__
         }
         out[d] = (int16_t)acc;
     }
+}
+
+// grid (width1, H), block 256 over d
+__global__ __launch_bounds__(256) void k_ocv_pixcost(const uint8_t* __restrict__ planes, Geom g,
+                                                     int16_t* __restrict__ cost)
+{
+    pixcost_cell(planes, g, blockIdx.x, blockIdx.y, cost);
 }
 
 // thread per (y, d): running horizontal box along x
@@ -251,6 +259,11 @@ __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__
 // value of row max(H - SH2 - 1, 0) in MODE_SGBM, or are P2 in MODE_HH). A thread owns two
 // adjacent disparities (one u32 of the row: width1 * D is even), int sums per half (the
 // overflow flag needs the true value), one u32 load per row and window edge, one u32 store.
+// SGM_OCV_COL0_LEGACY (OpenCV 3.x, `for (x = D; ...)`): column 0 keeps its row-0 value for
+// y >= 1 (MODE_SGBM's single C row) or the P2 initialisation (MODE_HH's per-row C).
+// Overflow flag (Geom::wide == 2): a C' above g.ovf_thr (32767: int16 volumes no longer exact
+// for the scalar branch; 32767 - P2 for SIMD_SAT, where (short)(minLr + P2) could wrap), or a
+// horizontal sum that left int16 (its u16 word has the sign bit: every true sum is >= 0).
 #ifndef SGM_VSUM_ROWS
 #define SGM_VSUM_ROWS 64
 #endif
@@ -267,18 +280,24 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
     const int y0 = blockIdx.y * kVsumRows, y1 = min(H, y0 + kVsumRows);
     auto lo16 = [](uint32_t w) { return (int)(int16_t)(uint16_t)w; };
     auto hi16 = [](uint32_t w) { return (int)w >> 16; };
+    uint32_t signs = 0;                                    // OR of every loaded sum word
     auto window = [&](int y, int& s0, int& s1) {
         s0 = 0; s1 = 0;
         for (int k = y - SH2; k <= y + SH2; k++) {
             const uint32_t w = h32[(size_t)min(max(k, 0), H - 1) * rs + i];
             s0 += lo16(w); s1 += hi16(w);
+            signs |= w;
         }
     };
-    bool ovf = false;                                      // a C' above int16 (Geom::wide == 2)
+    bool ovf = false;                                      // a C' above ovf_thr (Geom::wide == 2)
     const int ylast = max(H - SH2 - 1, 0);                 // last row whose window is recomputed
     const bool tail = y1 - 1 >= 1 && y1 - 1 + SH2 >= H;    // the segment reaches the repeated rows
     int rep0 = g.P2, rep1 = g.P2;
     if (!fullDP && tail) { int t0, t1; window(ylast, t0, t1); rep0 += t0; rep1 += t1; }
+    // column 0 under COL0_LEGACY: every row y >= 1 holds z (row 0's value, or P2 in MODE_HH)
+    const bool c0 = (g.compat & SGM_OCV_COL0_LEGACY) && i < g.D / 2;
+    int z0 = g.P2, z1 = g.P2;
+    if (c0 && !fullDP) { int t0, t1; window(0, t0, t1); z0 += t0; z1 += t1; }
     int s0, s1;
     window(y0, s0, s1);
     // rows in chunks of 8: the chunk's 16 entering / leaving rows are loaded together (clamped
@@ -291,6 +310,7 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
             const int y = min(yb + u, y1 - 1);
             ha[u] = h32[(size_t)min(y + SH2, H - 1) * rs + i];
             hb[u] = h32[(size_t)max(y - SH2 - 1, 0) * rs + i];
+            signs |= ha[u];
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -303,13 +323,79 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_seg(const int16_t* __restrict_
             } else {
                 v0 = rep0; v1 = rep1;
             }
-            ovf |= max(v0, v1) > kMaxCost;
+            if (c0 && y > 0) { v0 = z0; v1 = z1; }
+            ovf |= max(v0, v1) > g.ovf_thr;
             C32[(size_t)y * rs + i] = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
         }
     }
+    ovf |= (signs & 0x80008000u) != 0;
     if (g.wide == 2 && g.ovf) {                            // one atomic per wave that saw one
         const uint64_t b = __ballot(ovf);
         if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(g.ovf, 1);
+    }
+}
+
+// ---- SGM_OCV_SIMD_SAT frames the overflow flag marks: OpenCV's SIMD cost loop, exactly ------
+// (gated: each kernel returns at once unless the frame takes the flagged path). The SIMD
+// branch saturates the running sums of rows y >= 1 — the horizontal sums of image rows
+// k > SH2 ((h - sub) + add) and the vertical update ((Cprev - hsumSub) + hsumAdd) — so a value
+// that saturated once changes every later one: sequential sums, one thread per (row, d) or per
+// (column, d) pair; rows k <= SH2 and row y = 0 keep the scalar int16 wrap.
+// grid-stride over the (x1, y) cells of the frame, block 256 over d
+__global__ __launch_bounds__(256) void k_ocv_pixcost_sat(const uint8_t* __restrict__ planes, Geom g,
+                                                         int16_t* __restrict__ cost)
+{
+    if (!ocv_flagged(g)) return;
+    const int n = g.width1 * g.H;
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+        const int y = it / g.width1;
+        pixcost_cell(planes, g, it - y * g.width1, y, cost);
+    }
+}
+
+// thread per (image row k, d): the running horizontal box along x
+__global__ __launch_bounds__(256) void k_ocv_hsum_sat(const int16_t* __restrict__ pix, Geom g, int16_t* __restrict__ hs)
+{
+    if (!ocv_flagged(g)) return;
+    const int d = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+    if (d >= g.D) return;
+    const size_t rb = (size_t)k * g.width1 * g.D + d;
+    const int W1 = g.width1, SW2 = g.SW2;
+    int s = pix[rb] * (SW2 + 1);
+    for (int i = 1; i <= SW2; i++) s += pix[rb + (size_t)min(i, W1 - 1) * g.D];
+    int h = (int16_t)s;                                   // first column: scalar, int16 store
+    hs[rb] = (int16_t)h;
+    const bool sat = k > g.SH2;                            // computed for an output row y >= 1
+    for (int x = 1; x < W1; x++) {
+        const int a = pix[rb + (size_t)min(x + SW2, W1 - 1) * g.D];
+        const int b = pix[rb + (size_t)max(x - SW2 - 1, 0) * g.D];
+        h = sat ? sat16(sat16(h - b) + a) : (int)(int16_t)(h + a - b);
+        hs[rb + (size_t)x * g.D] = (int16_t)h;
+    }
+}
+
+// thread per (column, d): C' down the rows (OpenCV's row loop with the SIMD vertical update)
+__global__ __launch_bounds__(256) void k_ocv_vsum_sat(const int16_t* __restrict__ hs, Geom g, int fullDP,
+                                                      int16_t* __restrict__ C)
+{
+    if (!ocv_flagged(g)) return;
+    const size_t rc = (size_t)g.width1 * g.D;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rc) return;
+    const int H = g.H, SH2 = g.SH2;
+    const bool c0 = (g.compat & SGM_OCV_COL0_LEGACY) && i < (size_t)g.D;
+    int c = g.P2;                                          // row 0: P2 + the clamped window (int16 wrap)
+    for (int k = -SH2; k <= SH2; k++) c += hs[(size_t)min(max(k, 0), H - 1) * rc + i];
+    c = (int16_t)c;
+    C[i] = (int16_t)c;
+    for (int y = 1; y < H; y++) {
+        if (y + SH2 < H) {
+            if (!c0) c = sat16(sat16(c - hs[(size_t)max(y - SH2 - 1, 0) * rc + i]) + hs[(size_t)(y + SH2) * rc + i]);
+            else if (fullDP) c = g.P2;
+        } else if (fullDP) {
+            c = g.P2;                                      // MODE_HH: never recomputed, the P2 init
+        }                                                  // MODE_SGBM: the last computed row
+        C[(size_t)y * rc + i] = (int16_t)c;
     }
 }
 
@@ -486,15 +572,18 @@ __device__ __forceinline__ int line_shl1(int v, int p)
     return p == LPL - 1 ? kMaxCost : t;
 }
 // Lout: the CostType (int16) path costs, the recurrence's state; Lraw: the int values
-// OpenCV adds into S (equal to Lout unless a cost left int16)
-template <int DPL, int LPL>
+// OpenCV adds into S (equal to Lout unless a cost left int16).
+// SAT (SGM_OCV_SIMD_SAT in the overflow regime): the SIMD recurrence, all in saturating int16 —
+// Lp(d +- 1) + P1 saturated, delta = (short)(minLr + P2) (wraps), L = sat(sat(min - delta) + C);
+// Lout = Lraw = L and the min is over the int16 values.
+template <int DPL, int LPL, bool SAT = false>
 __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DPL], int mLp, bool pv, int p,
                                         const Geom& g, int (&Lout)[DPL], int (&Lraw)[DPL])
 {
     const int fromLeft = line_shr1<LPL>(Lp[DPL - 1], p);
     const int fromRight = line_shl1<LPL>(Lp[0], p);
     const int lp_min = pv ? mLp : 0;
-    const int delta = lp_min + g.P2;
+    const int delta = SAT ? (int)(int16_t)(lp_min + g.P2) : lp_min + g.P2;
     int lmin = 1 << 30;
 #pragma unroll
     for (int k = 0; k < DPL; k++) {
@@ -503,7 +592,13 @@ __device__ __forceinline__ int ocv_step(const int (&Cp)[DPL], const int (&Lp)[DP
         int lm1 = k > 0 ? Lp[k - 1] : fromLeft;
         int lp1 = k < DPL - 1 ? Lp[k + 1] : fromRight;
         if (!pv) { lm1 = d > 0 ? 0 : kMaxCost; lp1 = d < g.D - 1 ? 0 : kMaxCost; }
-        const int v = Cp[k] + min(a, min(lm1 + g.P1, min(lp1 + g.P1, delta))) - delta;
+        int v;
+        if constexpr (SAT) {
+            const int m = min(min(a, sat16(lm1 + g.P1)), min(sat16(lp1 + g.P1), delta));
+            v = sat16(sat16(m - delta) + Cp[k]);
+        } else {
+            v = Cp[k] + min(a, min(lm1 + g.P1, min(lp1 + g.P1, delta))) - delta;
+        }
         Lout[k] = d < g.D ? (int)(int16_t)v : kMaxCost;   // Lr is CostType (int16)
         Lraw[k] = d < g.D ? v : kMaxCost;
         if (d < g.D) lmin = min(lmin, v);                  // minL over the int values
@@ -541,12 +636,12 @@ constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 // line - width1 + 1. The lines of a block have (nearly) equal lengths; each stores only
 // while its own steps last. Fewer, wider lines (LPL 32) shorten each step's instruction
 // chain: a line is a sequential walk, and its step latency bounds the kernel.
-template <int DPL, int LPL, typename VT>
+template <int DPL, int LPL, typename VT, bool SAT>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, VT* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
                                                   int4 nblk1, int use_buf)
 {
-    if (ocv_gate_skip<VT>(g)) return;
+    if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
     // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
     int b = blockIdx.x, dir = 0, slot = 0;
@@ -619,7 +714,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             for (int q = 0; q < PF; q++) {
                 const int i = i0 + q;
                 int L[DPL], Lraw[DPL];
-                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
+                const int lmin = ocv_step<DPL, LPL, SAT>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
                 const bool ok = lane_act && i < n;
                 if constexpr (DPL == 32) {        // two halves: the straddling lane drops its upper one
                     const int (&Vs)[32] = kRaw ? Lraw : L;
@@ -659,7 +754,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             for (int q = 0; q < PF; q++) {
                 const int i = i0 + q;
                 int L[DPL], Lraw[DPL];
-                const int lmin = ocv_step<DPL, LPL>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
+                const int lmin = ocv_step<DPL, LPL, SAT>(Cb[q], Lp, mLp, !(decltype(first)::value && q == 0), p, g, L, Lraw);
                 const bool ok = lane_act && i < n;
                 if constexpr (DPL == 32) {
                     const int (&Vs)[32] = kRaw ? Lraw : L;
@@ -683,17 +778,55 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     }
 }
 
+// S of one cell from the direction volumes (slot order: MODE_SGBM dirs 0, 2, 3, 6, 7; MODE_HH
+// dirs 0..7), in OpenCV's order. Scalar branch: the int sum of pass 1 (dirs 6, 2, 0, 3 =
+// OpenCV's r0..r3) saturated, then the fifth path (MODE_SGBM) or pass 2 (dirs 7, 4, 1, 5),
+// saturated. SAT (SIMD branch): S = sat(sat(S + sat(L0 + L1)) + sat(L2 + L3)) per pass, the
+// fifth path sat(S + L).
+template <int NDIR, bool SAT, int DPL>
+__device__ __forceinline__ int ocv_sum(const int (&v)[NDIR][DPL], int k)
+{
+    if constexpr (SAT) {
+        if constexpr (NDIR == 5) {
+            const int s1 = sat16(sat16(v[3][k] + v[1][k]) + sat16(v[0][k] + v[2][k]));
+            return sat16(s1 + v[4][k]);
+        } else {
+            const int s1 = sat16(sat16(v[6][k] + v[2][k]) + sat16(v[0][k] + v[3][k]));
+            return sat16(sat16(s1 + sat16(v[7][k] + v[4][k])) + sat16(v[1][k] + v[5][k]));
+        }
+    } else {
+        int s1, s2;
+        if constexpr (NDIR == 5) {
+            s1 = v[0][k] + v[1][k] + v[2][k] + v[3][k];
+            s2 = v[4][k];
+        } else {
+            s1 = v[0][k] + v[2][k] + v[3][k] + v[6][k];
+            s2 = v[1][k] + v[4][k] + v[5][k] + v[7][k];
+        }
+        return sat16(sat16(s1) + s2);
+    }
+}
+
+// WTA key tie order: the first d (OpenCV 4.x / scalar), or SGM_OCV_LANE_TIE (3.x SSE2 MODE_SGBM:
+// lane d mod 8 first, then d) — `bits` = the key's disparity field width
+__device__ __forceinline__ int wta_tie(int d, bool lane, int bits) { return lane ? ((d & 7) << (bits - 3)) | (d >> 3) : d; }
+__device__ __forceinline__ int wta_untie(int t, bool lane, int bits)
+{
+    return lane ? ((t & ((1 << (bits - 3)) - 1)) << 3) | (t >> (bits - 3)) : t;
+}
+
 // WTA of the OCV modes, one workgroup (4 waves) per image row, 16 lanes per pixel (4 pixels
 // per wave-instruction): lane p of a row holds d = p*DPL .. p*DPL + DPL - 1 of its pixel,
 // loaded as one DPL-value vector per volume (coalesced). Same decisions as OpenCV's loop
 // (SURVEY Appendix A.6): S = the saturating sums in OpenCV's pass order; best = first minimal d through
 // one 16-lane min over (S + 32768) * 512 + d; uniqueness per element (S may be any int16
 // here); S[best +- 1] through a per-row LDS slice; then the shared disp2 / LR epilogue.
-template <int DPL, int NDIR, typename VT>
+template <int DPL, int NDIR, typename VT, bool SAT>
 __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, size_t vol_elems, Geom g,
                                                    int16_t* __restrict__ out, size_t out_stride)
 {
-    if (ocv_gate_skip<VT>(g)) return;
+    if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
+    const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
     extern __shared__ uint32_t lds_ocv[];
     int16_t* sl = (int16_t*)lds_ocv;                      // 16 lane rows x 16 lanes x DPL S values
     RowLds R((char*)lds_ocv + (size_t)16 * 16 * DPL * 2, g.W);
@@ -721,28 +854,17 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, 
         // (MODE_SGBM) or pass 2 (MODE_HH) — they differ once sums overflow int16
         int S[DPL];
 #pragma unroll
-        for (int k = 0; k < DPL; k++) {
-            int s1, s2;
-            if constexpr (NDIR == 5) {
-                s1 = nxt[0][k] + nxt[1][k] + nxt[2][k] + nxt[3][k];
-                s2 = nxt[4][k];
-            } else {
-                s1 = nxt[0][k] + nxt[2][k] + nxt[3][k] + nxt[6][k];
-                s2 = nxt[1][k] + nxt[4][k] + nxt[5][k] + nxt[7][k];
-            }
-            s1 = min(max(s1, -32768), 32767);
-            S[k] = min(max(s1 + s2, -32768), 32767);
-        }
+        for (int k = 0; k < DPL; k++) S[k] = ocv_sum<NDIR, SAT>(nxt, k);
         load(min(q + 4, nq - 1), nxt);
         uint32_t km = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < DPL; k++) {
             const int d = p * DPL + k;
-            const uint32_t key = ((uint32_t)(S[k] + 32768) << 9) | (uint32_t)d;
+            const uint32_t key = ((uint32_t)(S[k] + 32768) << 9) | (uint32_t)wta_tie(d, lanetie, 9);
             km = (lane_act && d < g.D) ? min(km, key) : km;
         }
         const uint32_t kmin = row_min_u32(km);
-        const int best = (int)(kmin & 511u);
+        const int best = wta_untie((int)(kmin & 511u), lanetie, 9);
         const int minS = (int)(kmin >> 9) - 32768;
         bool hit = false;
 #pragma unroll
@@ -776,11 +898,12 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, 
 // stores S in the wave's LDS slice; pass 2 reads the slice for the uniqueness test and
 // S[best +- 1]. Same decisions and the same disp2 / LR epilogue as k_ocv_wta16.
 constexpr int kWta64Chunk = 1024;
-template <int NDIR, typename VT>
+template <int NDIR, typename VT, bool SAT>
 __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, size_t vol_elems, Geom g,
                                                    int16_t* __restrict__ out, size_t out_stride)
 {
-    if (ocv_gate_skip<VT>(g)) return;
+    if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
+    const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
     constexpr int DPL = kWta64Chunk / 64;
     extern __shared__ uint32_t lds_ocv[];
     const int Dpad = (g.D + kWta64Chunk - 1) / kWta64Chunk * kWta64Chunk;
@@ -802,24 +925,15 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
             for (int k = 0; k < NDIR; k++) load_vals<VT, DPL>(base + (size_t)k * vol_elems, v[k]);
 #pragma unroll
             for (int k = 0; k < DPL; k++) {
-                int s1, s2;
-                if constexpr (NDIR == 5) {
-                    s1 = v[0][k] + v[1][k] + v[2][k] + v[3][k];
-                    s2 = v[4][k];
-                } else {
-                    s1 = v[0][k] + v[2][k] + v[3][k] + v[6][k];
-                    s2 = v[1][k] + v[4][k] + v[5][k] + v[7][k];
-                }
-                s1 = min(max(s1, -32768), 32767);
-                const int S = min(max(s1 + s2, -32768), 32767);
+                const int S = ocv_sum<NDIR, SAT>(v, k);
                 const int d = db + k;
-                const int key = ((S + 32768) << 11) | d;
+                const int key = ((S + 32768) << 11) | wta_tie(d, lanetie, 11);
                 km = (act && d < g.D) ? min(km, key) : km;
                 if (act) srow[d] = (int16_t)S;
             }
         }
         const int kmin = wave_min(km);
-        const int best = kmin & 2047;
+        const int best = wta_untie(kmin & 2047, lanetie, 11);
         const int minS = (kmin >> 11) - 32768;
         bool hit = false;
         for (int d = lane; d < g.D; d += 64)
@@ -842,6 +956,9 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
 // ------------------------------------------------------------------------------------
 static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
+// C' of the frame into bufA. SIMD_SAT frames that take the flagged kernels (Geom::wide != 0 and
+// the overflow flag) get the exact SIMD cost, sequential, into bufB (pixel costs -> bufB,
+// horizontal sums -> bufA, C' -> bufB): ocv_cost_buffer() says which one the paths read.
 hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, const Geom& g, int fullDP,
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
 {
@@ -858,11 +975,17 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
     }
     hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D / 2 + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows), dim3(256),
                        0, st, bufB, g, fullDP, bufA);
+    if (g.wide && (g.compat & SGM_OCV_SIMD_SAT)) {
+        const size_t rc = (size_t)g.width1 * g.D;
+        hipLaunchKernelGGL(k_ocv_pixcost_sat, dim3(std::min(g.width1 * g.H, 8192)), dim3(256), 0, st, planes, g, bufB);
+        hipLaunchKernelGGL(k_ocv_hsum_sat, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufB, g, bufA);
+        hipLaunchKernelGGL(k_ocv_vsum_sat, dim3((unsigned)((rc + 255) / 256)), dim3(256), 0, st, bufA, g, fullDP, bufB);
+    }
     return hipGetLastError();
 }
 
 // vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 VT of trash slots
-template <int DPL, int LPL, typename VT>
+template <int DPL, int LPL, typename VT, bool SAT>
 static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, const Geom& g, int dirmask,
                                hipStream_t st)
 {
@@ -883,17 +1006,21 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
     // 32-bit buffer offsets when a volume ends below kBufDrop (the shipped 2448x2048 D=480
     // config's int16 volumes are 3.6 GB; SGM_OCV_NO_BUF=1 forces the 64-bit path)
     const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < (size_t)kBufDrop && !getenv("SGM_OCV_NO_BUF");
-    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
+    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf);
 }
 
+// the plain kernels (wide != 1) and the flagged ones (wide != 0): int32 volumes for the scalar
+// branch, saturating int16 over the SIMD cost (Csat) for SIMD_SAT; with wide == 2 the one not
+// matching the frame's flag exits at once
 template <int DPL, int LPL>
-static void launch_ocv_paths_v(const int16_t* C, void* vols, size_t cells, const Geom& g, int dirmask,
-                               hipStream_t st)
+static void launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
+                               int dirmask, hipStream_t st)
 {
-    // gated (wide == 2): both launches, the one not matching *g.ovf exits at once
-    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t>(C, vols, cells, g, dirmask, st);
-    if (g.wide != 0) launch_ocv_paths_l<DPL, LPL, int32_t>(C, vols, cells, g, dirmask, st);
+    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st);
+    if (g.wide == 0) return;
+    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st);
+    else launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
@@ -917,32 +1044,32 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
     return waves < kOcvWideLineWaves ? 32 : 16;
 }
 
-hipError_t launch_ocv_paths(const int16_t* C, void* vols, size_t cells, const Geom& g, int dirmask,
-                            hipStream_t st)
+hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
+                            int dirmask, hipStream_t st)
 {
     const int D = g.D;
     const int lpl = ocv_lanes_per_line(g, dirmask);
     if (lpl == 64) {
-        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, vols, cells, g, dirmask, st);
-        else launch_ocv_paths_v<32, 64>(C, vols, cells, g, dirmask, st);
+        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st);
     } else if (lpl == 32) {
-        if (D <= 64) launch_ocv_paths_v<2, 32>(C, vols, cells, g, dirmask, st);
-        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, vols, cells, g, dirmask, st);
-        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, vols, cells, g, dirmask, st);
-        else launch_ocv_paths_v<16, 32>(C, vols, cells, g, dirmask, st);
+        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_v<1, 16>(C, vols, cells, g, dirmask, st); break;
-        case 2: launch_ocv_paths_v<2, 16>(C, vols, cells, g, dirmask, st); break;
-        case 4: launch_ocv_paths_v<4, 16>(C, vols, cells, g, dirmask, st); break;
-        case 8: launch_ocv_paths_v<8, 16>(C, vols, cells, g, dirmask, st); break;
-        default: launch_ocv_paths_v<16, 16>(C, vols, cells, g, dirmask, st); break;   // D <= 256 here
+        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st); break;   // D <= 256 here
         }
     }
     return hipGetLastError();
 }
 
-template <int DPL, typename VT>
+template <int DPL, typename VT, bool SAT>
 static void launch_ocv_wta_dpl(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                                size_t out_stride, hipStream_t st)
 {
@@ -950,12 +1077,12 @@ static void launch_ocv_wta_dpl(const void* vols, size_t cells, int ndir, const G
     const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
     const VT* v = (const VT*)vols;
     if (ndir == 8)
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
     else
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
 }
 
-template <typename VT>
+template <typename VT, bool SAT>
 static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                              size_t out_stride, hipStream_t st)
 {
@@ -965,25 +1092,28 @@ static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geo
         const size_t lds = (size_t)4 * ((D + kWta64Chunk - 1) / kWta64Chunk * kWta64Chunk) * 2 + RowLds::bytes(g.W);
         const VT* v = (const VT*)vols;
         if (ndir == 8)
-            hipLaunchKernelGGL((k_ocv_wta64<8, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+            hipLaunchKernelGGL((k_ocv_wta64<8, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
         else
-            hipLaunchKernelGGL((k_ocv_wta64<5, VT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+            hipLaunchKernelGGL((k_ocv_wta64<5, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
         return;
     }
-    if (D <= 32) launch_ocv_wta_dpl<2, VT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 64) launch_ocv_wta_dpl<4, VT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 128) launch_ocv_wta_dpl<8, VT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 256) launch_ocv_wta_dpl<16, VT>(vols, cells, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_dpl<32, VT>(vols, cells, ndir, g, out, out_stride, st);
+    if (D <= 32) launch_ocv_wta_dpl<2, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 64) launch_ocv_wta_dpl<4, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 128) launch_ocv_wta_dpl<8, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 256) launch_ocv_wta_dpl<16, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_dpl<32, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
 }
 
-// vols: int16 volumes (wide 0), int32 (wide 1), or an int32-sized region read as the one
-// the cost kernel's overflow flag selects (wide 2); cells = width1 * H * D per volume
+// vols: int16 volumes (wide 0), the flagged kind (wide 1: int32, or saturating int16 under
+// SIMD_SAT), or a region sized for the larger, read as the one the cost kernel's overflow
+// flag selects (wide 2); cells = width1 * H * D per volume
 hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                           size_t out_stride, hipStream_t st)
 {
-    if (g.wide != 1) launch_ocv_wta_t<int16_t>(vols, cells, ndir, g, out, out_stride, st);
-    if (g.wide != 0) launch_ocv_wta_t<int32_t>(vols, cells, ndir, g, out, out_stride, st);
+    if (g.wide != 1) launch_ocv_wta_t<int16_t, false>(vols, cells, ndir, g, out, out_stride, st);
+    if (g.wide == 0) return hipGetLastError();
+    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_wta_t<int16_t, true>(vols, cells, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_t<int32_t, false>(vols, cells, ndir, g, out, out_stride, st);
     return hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ hipError_t launch_depth_points(const float*, size_t, int, int, const float*, dou
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
-hipError_t launch_ocv_paths(const int16_t*, void*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t);
 hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
 }  // namespace sgm
 
@@ -102,7 +102,14 @@ int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
         // only frames with such a value take the int32 volumes (Geom::wide == 2): real images
         // stay far below the bound (the reference launch config, block 21: bound 41 413).
         // SGM_OCV_WIDE=1 forces int32 volumes; SGM_OCV_GATE=0 takes them whenever the bound allows.
-        const long long cmax = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63) + g.P2;
+        // The SIMD branches (ocv_compat SGM_OCV_SIMD_SAT) saturate instead, and agree with the
+        // plain kernels until a C' exceeds 32767 - P2 (then (short)(minLr + P2) can wrap): their
+        // flagged kernels are the sequential saturating cost and saturating int16 paths / sums.
+        g.compat = p.ocv_compat & (SGM_OCV_COL0_LEGACY | SGM_OCV_SIMD_SAT | SGM_OCV_LANE_TIE);
+        const bool sat = (g.compat & SGM_OCV_SIMD_SAT) != 0;
+        g.ovf_thr = sat ? 32767 - g.P2 : 32767;
+        const long long cmax = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63) + g.P2 +
+                               (sat ? g.P2 : 0);
         const char* wide_env = std::getenv("SGM_OCV_WIDE");
         const char* gate_env = std::getenv("SGM_OCV_GATE");
         if (wide_env && std::atoi(wide_env) != 0) g.wide = 1;
@@ -327,7 +334,9 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
     if (p.mode == SGM_MODE_CENSUS8) {
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
-        if (const char* e = std::getenv("SGM_VOL_PAD")) l.vol_bytes = align_up(l.vol_bytes + (size_t)std::atoll(e));
+        // extra bytes per volume slot (a measurement knob): clamped to [0, 1 GiB]
+        if (const char* e = std::getenv("SGM_VOL_PAD"))
+            l.vol_bytes = align_up(l.vol_bytes + (size_t)std::min(std::max(std::atoll(e), 0LL), 1LL << 30));
         l.group = std::max(group, 1);
         // D > 256 (32 disparities per lane, 2 waves/SIMD) keeps the earlier scheme: its up+WTA
         // blocks are long latency-bound chains (C5 batch: 32.3 vs 23.3 ms per frame)
@@ -352,7 +361,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.planes = take(WH * 4);
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
-        const size_t es = g.wide ? 4 : 2;          // int32 / int16 path volumes (Geom::wide)
+        const size_t es = g.wide && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // int32 / int16 path volumes
         // + slack: the path kernel's trash slots (64 lanes x 32 values) and the WTA's last pixel
         // group of the last row, which reads 3 pixels past the volume
         l.ovols = take(es * (sgm::ocv_vol_elems(cells, es) * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 64 * 32 +
@@ -493,11 +502,11 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
             gg.ovf = (int*)(ws + l.ovf);
             HIP_TRY(hipMemsetAsync(gg.ovf, 0, sizeof(int), st), "hipMemsetAsync");
         }
-        const double es = g.wide == 1 ? 4 : 2;   // gated: the int16 case (real images)
+        const double es = g.wide == 1 && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // gated: the int16 case
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
         HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, gg, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
         rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
-        HIP_TRY(sgm::launch_ocv_paths(A, V, ncells, gg, mask, st), "ocv_paths");
+        HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
         rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
         HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
     }
@@ -691,8 +700,12 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
 
 // OCV-mode batch (sgm_match_device_batch on an OpenCV mode): frames dealt round-robin over
 // S same-device lanes (own stream + workspace each; SGM_OCV_STREAMS, default 4, 1 = one
-// frame after another on the handle's stream). Every lane starts after the work already on
-// h->stream, and h->stream waits for every lane, so the call keeps the single-stream contract.
+// frame after another on the handle's stream). Lane 0 is h itself (its workspace is the one
+// the caller prepared); lanes 1.. are sub-handles, opened only while the device's free memory
+// holds their workspace (the shipped 2448x2048 D=480 block-21 frame needs 27-70 GB per
+// workspace, by mode and OpenCV build), and a lane whose allocation fails ends the list. Every
+// lane starts after the work already on h->stream, and h->stream waits for every lane, so the
+// call keeps the single-stream contract.
 int ocv_batch_lanes(int n)
 {
     const char* e = std::getenv("SGM_OCV_STREAMS");
@@ -700,34 +713,48 @@ int ocv_batch_lanes(int n)
     return std::max(1, std::min({s, n, 8}));
 }
 
-int run_batch_ocv(sgm_handle* h, int W, int H, const uint8_t* const* dLs, const uint8_t* const* dRs, int n,
-                  size_t stride, int16_t* const* outs, size_t out_stride)
+int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H, const uint8_t* const* dLs,
+                  const uint8_t* const* dRs, int n, size_t stride, int16_t* const* outs, size_t out_stride)
 {
-    const int S = ocv_batch_lanes(n);
-    while ((int)h->par.size() < S) h->par.push_back(nullptr);
-    if (!h->par_ev) HIP_TRY(hipEventCreateWithFlags(&h->par_ev, hipEventDisableTiming), "hipEventCreate");
-    std::vector<Geom> g(S);
-    std::vector<Layout> l(S);
-    for (int s = 0; s < S; s++) {
-        sgm_handle*& q = h->par[s];
-        if (!q) {
-            const int rc = sgm_create(&q, h->device);
-            if (rc) return fail(h, rc, "cannot open a batch lane");
-        }
+    const int Smax = ocv_batch_lanes(n);
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    const size_t reserve = std::max<size_t>(total_b / 64, (size_t)1 << 30);   // headroom for the caller
+    std::vector<Geom> g(1, g0);
+    std::vector<Layout> l(1, l0);
+    while ((int)h->par.size() < Smax - 1) h->par.push_back(nullptr);
+    int S = 1;
+    for (int s = 1; s < Smax; s++) {
+        sgm_handle*& q = h->par[s - 1];
+        const size_t have = q ? q->ws.size : 0;
+        const size_t extra = have >= l0.total ? 0 : l0.total;
+        if (extra + reserve > free_b) break;
+        if (!q && sgm_create(&q, h->device) != SGM_OK) break;
         q->params = h->params;
-        const int rc = prepare(q, W, H, false, g[s], l[s]);
-        if (rc) return fail(h, rc, q->err);
+        Geom gq;
+        Layout lq;
+        if (prepare(q, W, H, false, gq, lq) != SGM_OK) {   // e.g. an allocation failure: fewer lanes
+            q->err.clear();
+            break;
+        }
+        free_b -= std::min(free_b, extra);
+        g.push_back(gq);
+        l.push_back(lq);
+        S = s + 1;
     }
-    HIP_TRY(hipEventRecord(h->par_ev, h->stream), "hipEventRecord");
-    for (int s = 0; s < S; s++) HIP_TRY(hipStreamWaitEvent(h->par[s]->stream, h->par_ev, 0), "hipStreamWaitEvent");
+    if (S > 1) {
+        if (!h->par_ev) HIP_TRY(hipEventCreateWithFlags(&h->par_ev, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventRecord(h->par_ev, h->stream), "hipEventRecord");
+        for (int s = 1; s < S; s++) HIP_TRY(hipStreamWaitEvent(h->par[s - 1]->stream, h->par_ev, 0), "hipStreamWaitEvent");
+    }
     for (int i = 0; i < n; i++) {
-        sgm_handle* q = h->par[i % S];
-        const int rc = run_pipeline(q, l[i % S], g[i % S], dLs[i], dRs[i], stride, outs[i], out_stride);
-        if (rc) return fail(h, rc, q->err);
+        const int s = i % S;
+        sgm_handle* q = s ? h->par[s - 1] : h;
+        const int rc = run_pipeline(q, l[s], g[s], dLs[i], dRs[i], stride, outs[i], out_stride);
+        if (rc) return q == h ? rc : fail(h, rc, q->err);
     }
-    for (int s = 0; s < S; s++) {
-        sgm_handle* q = h->par[s];
-        if (!q->done) HIP_TRY(hipEventCreateWithFlags(&q->done, hipEventDisableTiming), "hipEventCreate");
+    for (int s = 1; s < S; s++) {
+        sgm_handle* q = h->par[s - 1];
         HIP_TRY(hipEventRecord(q->done, q->stream), "hipEventRecord");
         q->done_stream = q->stream;
         HIP_TRY(hipStreamWaitEvent(h->stream, q->done, 0), "hipStreamWaitEvent");
@@ -760,6 +787,7 @@ void sgm_default_params(sgm_params* p, int mode)
         p->min_disparity = 9; p->num_disparities = 64; p->block_size = 15; p->p1 = 200; p->p2 = 400;
         p->uniqueness_ratio = 15; p->disp12_max_diff = 0; p->prefilter_cap = 31; p->speckle_window_size = 100;
         p->speckle_range = 4; p->subpixel = 1; p->lr_check = 1; p->median = 1;
+        p->ocv_compat = SGM_OCV_COMPAT_MELODIC;   // the reference's Dockerfile:1 (melodic, OpenCV 3.2 SSE2)
     }
 }
 
@@ -889,7 +917,7 @@ int sgm_match_device_batch_rect(sgm_handle* h, const uint8_t* const* dLs, const 
     } else if (pipelined) {
         rc = run_batch_census(h, l, g, dLs, dRs, n, stride, outs, out_stride, rectLs, rectRs, rect_stride);
     } else if (h->params.mode != SGM_MODE_CENSUS8 && ocv_batch_lanes(n) > 1 && !h->profiling) {
-        rc = run_batch_ocv(h, W, H, dLs, dRs, n, stride, outs, out_stride);
+        rc = run_batch_ocv(h, l, g, W, H, dLs, dRs, n, stride, outs, out_stride);
     } else {
         for (int i = 0; i < n && rc == 0; i++) rc = run_pipeline(h, l, g, dLs[i], dRs[i], stride, outs[i], out_stride);
     }
@@ -1906,11 +1934,21 @@ int sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W,
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
     HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, h->stream), "H2D");
     int16_t* A = (int16_t*)(ws + l.bufA);
+    int16_t* B = (int16_t*)(ws + l.bufB);
+    int flag = 0;
+    if (g.wide == 2) {
+        g.ovf = (int*)(ws + l.ovf);
+        HIP_TRY(hipMemsetAsync(g.ovf, 0, sizeof(int), h->stream), "hipMemsetAsync");
+    }
     HIP_TRY(sgm::launch_ocv_cost((const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, g,
-                                 h->params.mode == SGM_MODE_OCV_HH8, (uint8_t*)(ws + l.planes), A,
-                                 (int16_t*)(ws + l.bufB), h->stream), "ocv_cost");
+                                 h->params.mode == SGM_MODE_OCV_HH8, (uint8_t*)(ws + l.planes), A, B, h->stream),
+            "ocv_cost");
+    if (g.wide == 2) HIP_TRY(hipMemcpyAsync(&flag, g.ovf, sizeof(int), hipMemcpyDeviceToHost, h->stream), "D2H flag");
+    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
+    // SIMD_SAT frames in the overflow regime: the sequential saturating cost (bufB)
+    const bool simd = (g.wide == 1 || (g.wide == 2 && flag)) && (g.compat & SGM_OCV_SIMD_SAT);
     const size_t cells = (size_t)g.width1 * g.H * g.D;
-    HIP_TRY(hipMemcpyAsync(cost, A, cells * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipMemcpyAsync(cost, simd ? B : A, cells * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
     return SGM_OK;
 }

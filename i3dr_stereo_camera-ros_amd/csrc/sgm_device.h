@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sgm_hip.h"
+
 #include <type_traits>
 
 namespace sgm {
@@ -38,10 +40,15 @@ struct Geom {
     int subpix, lr;         // census: subpixel / LR-check flags (OCV: 1, 1)
     int invalid;            // (minD - 1) * 16
     int SW2, SH2, ftzero;   // OCV: SAD half window, prefilter cap
-    int wide;               // OCV path volumes: 0 int16; 1 int32 (a cost may leave int16: exact S);
-                            // 2 gated: the cost kernel sets *ovf when a C' actually leaves
-                            // int16, and int16 / int32 launches each run only on their case
+    int wide;               // OCV overflow regime: 0 the plain int16 kernels; 1 the "flagged"
+                            // kernels (scalar branch: int32 path volumes, exact S; SIMD_SAT: the
+                            // sequential saturating cost + saturating int16 paths and sums);
+                            // 2 gated: the cost kernel sets *ovf when a frame needs the flagged
+                            // kernels, and both kinds are launched, each running only on its case
     int* ovf;               // device flag of wide == 2 (null otherwise)
+    int compat;             // OCV: SGM_OCV_* bits (sgm_params.ocv_compat); census: 0
+    int ovf_thr;            // OCV: largest C' the plain kernels reproduce exactly (32767, or
+                            // 32767 - P2 under SIMD_SAT: (short)(minLr + P2) must not wrap)
 };
 
 // Elements of one OCV path volume of `cells` cells at es bytes per cell (256-B aligned
@@ -69,12 +76,17 @@ __device__ __forceinline__ void lr_prio(int rem, int span)
     else __builtin_amdgcn_s_setprio(0);
 }
 
-// Gate of the wide == 2 launches: false when this launch's element type is not the one the
-// frame needs (uniform: a kernel argument and one scalar load).
-template <typename VT>
+// Gate of the wide == 2 launches: true when this launch's kind (FLAGGED: the overflow-regime
+// kernels) is not the one the frame needs (uniform: a kernel argument and one scalar load).
+template <bool FLAGGED>
 __device__ __forceinline__ bool ocv_gate_skip(const Geom& g)
 {
-    return g.wide == 2 && ((*g.ovf != 0) != (sizeof(VT) == 4));
+    return g.wide == 2 && ((*g.ovf != 0) != FLAGGED);
+}
+// The frame takes the flagged kernels (wide == 1 always, wide == 2 when the cost kernel said so)
+__device__ __forceinline__ bool ocv_flagged(const Geom& g)
+{
+    return g.wide == 1 || (g.wide == 2 && *g.ovf != 0);
 }
 
 // Direction r = (rx, ry): L_r(p) depends on L_r(p - r). Engine volume order.

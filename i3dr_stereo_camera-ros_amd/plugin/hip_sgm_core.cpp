@@ -2,9 +2,22 @@
 #include "hip_sgm_core.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <iostream>
 
 namespace sgm_hip {
+
+// SGM_HIP_OCV_COMPAT = melodic | noetic | scalar | <bits>: the OpenCV build the OCV modes
+// reproduce (include/sgm_hip.h SGM_OCV_*); unset: sgm_default_params' melodic default.
+int ocv_compat_from_env(int fallback)
+{
+    const char* e = std::getenv("SGM_HIP_OCV_COMPAT");
+    if (!e || !*e) return fallback;
+    if (!std::strcmp(e, "melodic")) return SGM_OCV_COMPAT_MELODIC;
+    if (!std::strcmp(e, "noetic")) return SGM_OCV_COMPAT_NOETIC;
+    if (!std::strcmp(e, "scalar")) return SGM_OCV_COMPAT_SCALAR;
+    return (int)std::strtol(e, nullptr, 0) & (SGM_OCV_COL0_LEGACY | SGM_OCV_SIMD_SAT | SGM_OCV_LANE_TIE);
+}
 
 MatcherCore::MatcherCore(int device, int mode) : device_(device)
 {
@@ -13,6 +26,7 @@ MatcherCore::MatcherCore(int device, int mode) : device_(device)
         mode = env ? std::atoi(env) : SGM_MODE_OCV_SGBM5;
     }
     sgm_default_params(&params_, mode);
+    params_.ocv_compat = ocv_compat_from_env(params_.ocv_compat);
     // cv::StereoSGBM::create(64, 9, 5) (matcherOpenCVSGBM.cpp:14): overwritten by the setters
     params_.min_disparity = 64;
     params_.num_disparities = 9;
@@ -39,6 +53,7 @@ void MatcherCore::setP1(float p1) { params_.p1 = (int)p1; }
 void MatcherCore::setP2(float p2) { params_.p2 = (int)p2; }
 void MatcherCore::setInterpolation(bool e) { interpolate_ = e; }
 void MatcherCore::setMode(int m) { params_.mode = m; }
+void MatcherCore::setOcvCompat(int bits) { params_.ocv_compat = bits; }
 
 sgm_params MatcherCore::rightMatcherParams(const sgm_params& p)
 {

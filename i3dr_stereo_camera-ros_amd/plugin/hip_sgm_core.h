@@ -16,6 +16,9 @@
 
 namespace sgm_hip {
 
+// SGM_HIP_OCV_COMPAT (melodic | noetic | scalar | <bits>), else `fallback`
+int ocv_compat_from_env(int fallback);
+
 class MatcherCore {
 public:
     // mode < 0: SGM_HIP_MODE env var, default SGM_MODE_OCV_SGBM5 (the reference's SGBM
@@ -38,6 +41,7 @@ public:
     void setP2(float p2);
     void setInterpolation(bool enable);
     void setMode(int mode);
+    void setOcvCompat(int bits);   // SGM_OCV_* (default: SGM_HIP_OCV_COMPAT env, else melodic)
 
     // --- matching -------------------------------------------------------------------
     // u8 mono rectified pair -> CV_32FC1-layout disparity in 1/16 px (x16 fixed point,

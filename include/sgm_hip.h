@@ -48,6 +48,25 @@ extern "C" {
 /* North-star mode: 9x7 census, Hamming cost, 8 directions, u8 path costs, u16 sums.       */
 #define SGM_MODE_CENSUS8      2
 
+/* OpenCV build variants of the OCV modes (`sgm_params.ocv_compat`, a bitfield). The reference
+ * pins OpenCV only through its ROS distro — melodic (OpenCV 3.2.0, the reference's Dockerfile:1,
+ * amd64) and noetic (OpenCV 4.2.0; CI matrix .github/workflows/ros-build.yml:14-21) — and
+ * computeDisparitySGBM differs between those releases and between its scalar and SIMD (SSE2 /
+ * universal-intrinsic, every x86-64 build) branches. Bits:
+ *   COL0_LEGACY  3.x cost loop: C' column 0 is never updated for rows y > 0
+ *   SIMD_SAT     saturating int16 box sums, path recurrence and S (SIMD branches)
+ *   LANE_TIE     3.x SSE2 MODE_SGBM WTA: among equal minimal sums the lowest lane (d mod 8) wins
+ * The three agree with the scalar restatement except on column 0 (COL0, every frame), on int16
+ * overflow (SIMD_SAT) and on exact cross-lane ties (LANE_TIE). Census mode ignores the field. */
+#define SGM_OCV_COL0_LEGACY   1
+#define SGM_OCV_SIMD_SAT      2
+#define SGM_OCV_LANE_TIE      4
+#define SGM_OCV_COMPAT_SCALAR   0                      /* the scalar 4.x restatement            */
+#define SGM_OCV_COMPAT_NOETIC   SGM_OCV_SIMD_SAT      /* noetic x86-64: OpenCV 4.2, SIMD        */
+#define SGM_OCV_COMPAT_MELODIC  (SGM_OCV_COL0_LEGACY | SGM_OCV_SIMD_SAT | SGM_OCV_LANE_TIE)
+                                                       /* melodic x86-64 (the Docker image): 3.2, SSE2;
+                                                        * the default of sgm_default_params      */
+
 /* Parameter block. Field names follow the reference's setters
  * (abstractStereoMatcher.h:27-48) and cfg/i3DR_Disparity.cfg:21-39.                      */
 typedef struct sgm_params {
@@ -65,6 +84,7 @@ typedef struct sgm_params {
     int subpixel;             /* census: parabolic 1/16 interpolation on/off (OCV: always on) */
     int lr_check;             /* census: left-right (disp2) check on/off (OCV: always on)     */
     int median;               /* census: 3x3 median post-filter on/off (OCV: always on)       */
+    int ocv_compat;           /* OCV modes: SGM_OCV_* bits of the OpenCV build to reproduce   */
 } sgm_params;
 
 typedef struct sgm_handle sgm_handle;
@@ -81,7 +101,8 @@ int  sgm_create(sgm_handle** out, int device);
 void sgm_destroy(sgm_handle* h);
 
 /* Defaults: census mode = north-star config (P1 10, P2 120, uniq 5, subpixel+LR on);
- * OCV modes = the generate_disparity node defaults (generate_disparity.cpp:100-112).      */
+ * OCV modes = the generate_disparity node defaults (generate_disparity.cpp:100-112) and
+ * ocv_compat = SGM_OCV_COMPAT_MELODIC (the OpenCV the reference's Dockerfile:1 ships).     */
 void sgm_default_params(sgm_params* p, int mode);
 
 /* Store parameters. Like the reference's setters this never fails on values; invalid

@@ -46,9 +46,10 @@ static inline int16_t sat16(int v) { return (int16_t)iclamp(v, SHRT_MIN, SHRT_MA
  * OpenCV build variants (oracle switches; DESIGN.md §3 "OpenCV semantics targets").
  * The reference pins OpenCV only by ROS distro (melodic -> 3.2.0, noetic -> 4.2.0;
  * .github/workflows/ros-build.yml:14-21, CMakeLists.txt:48-51), and computeDisparitySGBM
- * differs between versions and between its scalar and CV_SIMD branches. Default (0) is the
- * restatement the GPU engine reproduces: the scalar branch with the column-0 update of the
- * refactored 4.x loop. Bits:
+ * differs between versions and between its scalar and CV_SIMD branches. The bits come from
+ * `sgm_params.ocv_compat` (include/sgm_hip.h SGM_OCV_*; the GPU engine reproduces every
+ * combination), OR-ed with the process-wide switch below (the KATs' context manager).
+ * 0 is the scalar branch with the column-0 update of the refactored 4.x loop. Bits:
  *   SGMREF_OCV_COL0_LEGACY  the 3.x loop `for (x = D; x < width1*D; x += D)`: for y > 0 the
  *                           vertical running sum never updates C' column 0 (x = minX1), so it
  *                           keeps its row-0 value (MODE_SGBM, one C row buffer) or the P2
@@ -67,9 +68,9 @@ static inline int16_t sat16(int v) { return (int16_t)iclamp(v, SHRT_MIN, SHRT_MA
  *                           minimal S the winner is the one in the lowest lane (d mod 8), then
  *                           the smallest d in that lane, instead of the smallest d.
  * ====================================================================================== */
-#define SGMREF_OCV_COL0_LEGACY 1
-#define SGMREF_OCV_SIMD_SAT 2
-#define SGMREF_OCV_LANE_TIE 4
+#define SGMREF_OCV_COL0_LEGACY SGM_OCV_COL0_LEGACY
+#define SGMREF_OCV_SIMD_SAT SGM_OCV_SIMD_SAT
+#define SGMREF_OCV_LANE_TIE SGM_OCV_LANE_TIE
 static int g_ocv_compat = 0;
 void sgmref_set_ocv_compat(int flags) { g_ocv_compat = flags; }
 int sgmref_get_ocv_compat(void) { return g_ocv_compat; }
@@ -119,7 +120,7 @@ static int effective(const sgm_params* p, int width, int height, eff_t* e)
         e->subpix = 1; e->lr = 1; e->median = 1;
         e->npasses = p->mode == SGM_MODE_OCV_HH8 ? 2 : 1;
     }
-    e->compat = e->census ? 0 : g_ocv_compat;
+    e->compat = e->census ? 0 : ((p->ocv_compat | g_ocv_compat) & 7);
     e->uniq = p->uniqueness_ratio >= 0 ? p->uniqueness_ratio : 10;
     e->disp12 = p->disp12_max_diff > 0 ? p->disp12_max_diff : 1;
     e->minX1 = imax(e->maxD, 0);

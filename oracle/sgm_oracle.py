@@ -29,7 +29,7 @@ class SgmParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "mode", "min_disparity", "num_disparities", "block_size", "p1", "p2",
         "uniqueness_ratio", "disp12_max_diff", "prefilter_cap", "speckle_window_size",
-        "speckle_range", "subpixel", "lr_check", "median")]
+        "speckle_range", "subpixel", "lr_check", "median", "ocv_compat")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -37,15 +37,16 @@ class SgmParams(ctypes.Structure):
 
 def make_params(mode=MODE_CENSUS8, **kw):
     """Defaults mirror sgm_default_params(): census = north-star config; OCV = node defaults
-    (reference src/generate_disparity.cpp:100-112)."""
+    (reference src/generate_disparity.cpp:100-112) with ocv_compat = COMPAT_MELODIC (the
+    OpenCV 3.2 SSE2 build of the reference's Dockerfile:1)."""
     if mode == MODE_CENSUS8:
         d = dict(mode=mode, min_disparity=0, num_disparities=128, block_size=0, p1=10, p2=120,
                  uniqueness_ratio=5, disp12_max_diff=1, prefilter_cap=0, speckle_window_size=0,
-                 speckle_range=0, subpixel=1, lr_check=1, median=0)
+                 speckle_range=0, subpixel=1, lr_check=1, median=0, ocv_compat=0)
     else:
         d = dict(mode=mode, min_disparity=9, num_disparities=64, block_size=15, p1=200, p2=400,
                  uniqueness_ratio=15, disp12_max_diff=0, prefilter_cap=31, speckle_window_size=100,
-                 speckle_range=4, subpixel=1, lr_check=1, median=1)
+                 speckle_range=4, subpixel=1, lr_check=1, median=1, ocv_compat=COMPAT_MELODIC)
     d.update(kw)
     p = SgmParams()
     for k, v in d.items():
@@ -187,6 +188,9 @@ def filter_speckles(disp, new_val, max_size, max_diff):
 OCV_COL0_LEGACY = 1    # 3.x: the vertical running sum skips C' column 0 for y > 0
 OCV_SIMD_SAT = 2       # CV_SIMD branches: int16 saturating sums / recurrence / S
 OCV_LANE_TIE = 4       # MODE_SGBM SSE2 WTA: lowest lane (d mod 8) wins among equal minima
+COMPAT_SCALAR = 0                                          # the scalar 4.x restatement
+COMPAT_NOETIC = OCV_SIMD_SAT                               # noetic x86-64: OpenCV 4.2 SIMD
+COMPAT_MELODIC = OCV_COL0_LEGACY | OCV_SIMD_SAT | OCV_LANE_TIE  # melodic x86-64: OpenCV 3.2 SSE2
 
 
 class ocv_compat:

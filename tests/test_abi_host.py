@@ -47,6 +47,22 @@ def test_default_params_match_node_defaults(pkg):
             p.speckle_window_size, p.speckle_range, p.prefilter_cap) == (9, 64, 15, 200, 400, 15, 100, 4, 31)
     c = pkg.default_params(pkg.MODE_CENSUS8)
     assert (c.p1, c.p2, c.uniqueness_ratio, c.subpixel, c.lr_check) == (10, 120, 5, 1, 1)
+    # the OpenCV build the OCV modes reproduce: melodic (the reference's Dockerfile:1), census: n/a
+    assert p.ocv_compat == pkg.COMPAT_MELODIC == 7 and c.ocv_compat == 0
+    assert ctypes.sizeof(pkg.SgmParams) == 15 * 4
+
+
+@pytest.mark.parametrize("val,bits", [(None, 7), ("melodic", 7), ("noetic", 2), ("scalar", 0), ("5", 5),
+                                      ("0x3", 3)])
+def test_ocv_compat_env(pkg, monkeypatch, val, bits):
+    """SGM_HIP_OCV_COMPAT selects the OpenCV build, in the Python mirror's
+    MatcherHIPSGM like in the C++ adapter core."""
+    if val is None:
+        monkeypatch.delenv("SGM_HIP_OCV_COMPAT", raising=False)
+    else:
+        monkeypatch.setenv("SGM_HIP_OCV_COMPAT", val)
+    assert pkg.ocv_compat_from_env() == bits
+    assert pkg.MatcherHIPSGM(" ", (0, 0), mode=pkg.MODE_OCV_SGBM5).params.ocv_compat == bits
 
 
 @pytest.mark.parametrize("mode,D,expect", [("census", 64, 0), ("census", 24, -2), ("census", 0, -2),

@@ -4,7 +4,9 @@ Each case draws a mode (census, MODE_SGBM, MODE_HH), an image size (including he
 the SAD window and widths that leave no valid column), a disparity window (negative minD
 included), penalties, uniqueness (0, ordinary, >= 100), LR / subpixel / median / speckle
 settings and an image kind (textured stereo pair, noise, or pairs with flat patches that
-trip the uniqueness and speckle rules). The seeds are fixed, so a failure names a
+trip the uniqueness and speckle rules); OpenCV-mode cases also draw the OpenCV build variant
+(`ocv_compat`, all eight bit combinations) and sometimes binary 0/255 images whose box sums
+leave int16 (the overflow regime: int32 or saturating SIMD kernels). The seeds are fixed, so a failure names a
 reproducible configuration. Census cases also run through the pipelined device batch
 (`sgm_match_device_batch`) with a random frame count and through the exact row-band mode
 (`sgm_match_tiled_exact`) with a random band count.
@@ -24,6 +26,10 @@ N_CASES = int(os.environ.get("SGM_FUZZ_CASES", "120"))   # a longer hunt: SGM_FU
 def _images(rng, synth, h, w, minD, D, kind, seed):
     if kind == "noise":
         return (rng.integers(0, 256, (h, w), dtype=np.uint8), rng.integers(0, 256, (h, w), dtype=np.uint8))
+    if kind == "binary":        # 0/255 noise against its (partly) negated copy: maximal costs
+        left = (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8)
+        right = np.where(rng.random((h, w)) < 0.8, 255 - left, left).astype(np.uint8)
+        return left, right
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=seed, with_truth=False)
     if kind == "flat":
         left, right = left.copy(), right.copy()
@@ -57,6 +63,12 @@ def _case(pkg, seed):
         kw.update(p1=p1, p2=int(rng.integers(p1 + 1, 1200)), block_size=int(rng.choice([1, 3, 5, 7, 9, 11, 15, 21])),
                   prefilter_cap=int(rng.integers(1, 64)))
     kind = str(rng.choice(["pair", "pair", "noise", "flat"]))
+    if mode != pkg.MODE_CENSUS8:
+        kw["ocv_compat"] = int(rng.integers(0, 8))
+        if rng.random() < 0.2:
+            kind = "binary"
+            kw.update(block_size=int(rng.choice([15, 21, 31])), prefilter_cap=int(rng.integers(40, 64)),
+                      p2=int(rng.integers(kw["p1"] + 1, 6000)))
     return rng, mode, h, w, kw, kind
 
 

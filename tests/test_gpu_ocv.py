@@ -64,12 +64,17 @@ def test_ocv_node_defaults_c1(engine, oracle, synth, pkg, mode):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+COMPATS = pytest.mark.parametrize("compat", [0, 7], ids=["scalar", "melodic"])   # sgm_params.ocv_compat
+
+
+@COMPATS
 @pytest.mark.parametrize("nobuf", ["", "1"], ids=["buf32", "ptr64"])
 @pytest.mark.parametrize("lanes", ["16", "32"])
 @pytest.mark.parametrize("mode,h,w,minD,D,block", [(0, 480, 640, 9, 64, 15), (1, 96, 500, 0, 128, 5),
                                                    (0, 40, 600, -4, 256, 7), (1, 33, 200, 3, 48, 3),
                                                    (1, 24, 640, -3, 480, 9), (0, 20, 700, 147, 400, 21)])
-def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf, lanes, mode, h, w, minD, D, block):
+def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf, lanes, mode, h, w, minD, D, block,
+                                 compat):
     """Both path-kernel shapes (16 and 32 lanes per line, SGM_OCV_LPL) and both addressing
     schemes (32-bit buffer offsets; the 64-bit clamped pointers of > 2 GB volumes,
     SGM_OCV_NO_BUF) on the same inputs."""
@@ -77,7 +82,7 @@ def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf,
     if nobuf:
         monkeypatch.setenv("SGM_OCV_NO_BUF", nobuf)
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h + D)
-    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block)
+    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, ocv_compat=compat)
     engine.set_params(p)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
@@ -101,13 +106,15 @@ def test_ocv_saturated_sums(engine, oracle, pkg, mode, uniq):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@COMPATS
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("force", ["", "1"], ids=["auto", "forced"])
-def test_ocv_wide_path_costs(engine, oracle, synth, pkg, monkeypatch, mode, force):
+def test_ocv_wide_path_costs(engine, oracle, synth, pkg, monkeypatch, mode, force, compat):
     """Boxes whose sums can wrap int16 (21x21, preFilterCap 62): OpenCV's CostType cost
     volume wraps, a path cost can leave int16, and S adds the int values — the engine keeps
-    int32 path volumes there (Geom::wide, automatic from the parameters). `forced` runs an
-    ordinary configuration through the int32 volumes too (SGM_OCV_WIDE=1)."""
+    int32 path volumes there (Geom::wide, automatic from the parameters); the SIMD builds
+    (melodic) saturate instead: the sequential saturating cost + int16 saturating paths.
+    `forced` runs an ordinary configuration through those kernels too (SGM_OCV_WIDE=1)."""
     if force:
         monkeypatch.setenv("SGM_OCV_WIDE", force)
         kw = dict(min_disparity=-4, num_disparities=48, block_size=5)
@@ -119,7 +126,7 @@ def test_ocv_wide_path_costs(engine, oracle, synth, pkg, monkeypatch, mode, forc
         left = np.full((9, 118), 90, dtype=np.uint8)
         left[:, ::3] = rng.integers(0, 256, (9, 40), dtype=np.uint8)
         right = np.roll(left, -3, axis=1)
-    p = pkg.default_params(mode, speckle_window_size=0, **kw)
+    p = pkg.default_params(mode, speckle_window_size=0, ocv_compat=compat, **kw)
     engine.set_params(p)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
@@ -200,11 +207,13 @@ def test_plugin_core_cpp_init_and_match(tmp_path, oracle, synth):
     assert np.array_equal(got, oracle.match(oracle.make_params(0), left, right).astype(np.float32))
 
 
-@pytest.mark.parametrize("wide", ["", "1"], ids=["int16", "int32"])
+@COMPATS
+@pytest.mark.parametrize("wide", ["", "1"], ids=["plain", "flagged"])
 @pytest.mark.parametrize("mode,h,w,minD,D,block,spk", [(0, 20, 1400, 0, 1024, 5, 100), (1, 24, 1300, -7, 784, 3, 0),
                                                        (0, 12, 2300, 3, 2048, 7, 0), (1, 28, 2200, 0, 1536, 5, 0),
                                                        (0, 16, 1340, -1, 1296, 3, 10), (1, 20, 1200, 0, 1040, 5, 0)])
-def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wide, mode, h, w, minD, D, block, spk):
+def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wide, mode, h, w, minD, D, block, spk,
+                                    compat):
     """D > 512 in the OpenCV modes (the node's cfg allows disparity ranges up to 2048):
     64-lane path lines (16 or 32 values per lane; D % 32 = 16 above 1024 leaves one lane
     straddling D, found by the D > 512 fuzz) and the one-pixel-per-wave WTA in chunks of 1024
@@ -212,7 +221,8 @@ def test_ocv_large_disparity_ranges(engine, oracle, synth, pkg, monkeypatch, wid
     if wide:
         monkeypatch.setenv("SGM_OCV_WIDE", wide)
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), min(D, 256), seed=D + h)
-    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, speckle_window_size=spk)
+    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, speckle_window_size=spk,
+                           ocv_compat=compat)
     engine.set_params(p)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)

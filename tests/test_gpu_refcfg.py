@@ -91,3 +91,31 @@ def test_reference_config_full_frame_properties(engine, pkg, ref_frame, mode, mo
     # disparities inside the search window
     v = a[valid]
     assert v.min() >= 147 * 16 and v.max() <= (147 + 480) * 16
+
+
+@pytest.mark.parametrize("compat", [0, 7], ids=["scalar-int32", "melodic-int16"])
+def test_reference_config_hh_device_batch(engine, pkg, ref_frame, compat):
+    """The shipped 2448 x 2048 D=480 block-21 frame in MODE_HH through sgm_match_device_batch
+    with 5 frames: the same-device stream lanes are opened only while the free HBM
+    holds their workspaces (scalar build: int32 volumes, ~70 GB each; melodic: int16), with the
+    handle itself as lane 0; every frame equals its single match."""
+    torch = pytest.importorskip("torch")
+    left, right, _ = ref_frame
+    p = pkg.default_params(pkg.MODE_OCV_HH8, ocv_compat=compat, **REF_KW)
+    engine.set_params(p)
+    n = 5
+    ls = [np.ascontiguousarray(np.roll(left, 7 * i, axis=0)) for i in range(n)]
+    rs = [np.ascontiguousarray(np.roll(right, 7 * i, axis=0)) for i in range(n)]
+    dl = [torch.from_numpy(a).cuda() for a in ls]
+    dr = [torch.from_numpy(a).cuda() for a in rs]
+    out = torch.full((n, REF_H, REF_W), 777, dtype=torch.int16, device="cuda")
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    engine.match_device_batch([t.data_ptr() for t in dl], [t.data_ptr() for t in dr], REF_W, REF_H, REF_W,
+                              [out[i].data_ptr() for i in range(n)], REF_W, stream.cuda_stream)
+    stream.synchronize()
+    got = out.cpu().numpy()
+    del out, dl, dr
+    for i in (0, n - 1):
+        single = engine.match(ls[i], rs[i])
+        assert np.array_equal(got[i], single), f"frame {i}: {(got[i] != single).sum()} pixels differ"

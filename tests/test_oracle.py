@@ -111,8 +111,9 @@ def np_bt_cost(left, right, minD, D, ftzero):
     return cost
 
 
-def np_box_cost(pix, SW2, SH2, P2, fullDP):
-    """Exact replicate box sum + OpenCV's bottom-row rule + P2 offset."""
+def np_box_cost(pix, SW2, SH2, P2, fullDP, col0_legacy=False):
+    """Exact replicate box sum + OpenCV's bottom-row rule + P2 offset (+ the 3.x rule: column 0
+    of rows y >= 1 keeps row 0's value, or P2 in MODE_HH)."""
     H, W1, D = pix.shape
     xi = np.clip(np.arange(W1)[:, None] + np.arange(-SW2, SW2 + 1)[None, :], 0, W1 - 1)
     hs = pix[:, xi, :].sum(axis=2)
@@ -123,6 +124,8 @@ def np_box_cost(pix, SW2, SH2, P2, fullDP):
     for y in range(1, H):
         if y + SH2 >= H:
             C[y] = P2 if fullDP else C[last]
+    if col0_legacy:
+        C[1:, 0] = P2 if fullDP else C[0, 0]
     return C
 
 
@@ -183,18 +186,21 @@ def test_census_path_matches_numpy(oracle, synth, dirn, minD, D):
     assert np.array_equal(got.astype(np.int32), ref)
 
 
+@pytest.mark.parametrize("compat", [0, 1, 7])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("h,w,minD,D,block,cap", [(12, 50, 0, 16, 5, 31), (9, 45, 4, 16, 7, 15),
                                                   (4, 40, -3, 16, 9, 63), (17, 70, 2, 32, 3, 1)])
-def test_ocv_cost_matches_numpy(oracle, mode, h, w, minD, D, block, cap):
+def test_ocv_cost_matches_numpy(oracle, mode, h, w, minD, D, block, cap, compat):
+    """C' against a numpy box sum, for the scalar, 3.x-column-0 and melodic builds (no sum
+    leaves int16 here, so the SIMD saturation cannot show)."""
     rng = np.random.default_rng(h * w + mode)
     left = rng.integers(0, 256, (h, w), dtype=np.uint8)
     right = rng.integers(0, 256, (h, w), dtype=np.uint8)
     p = oracle.make_params(mode, min_disparity=minD, num_disparities=D, block_size=block, prefilter_cap=cap,
-                           p1=8, p2=32)
+                           p1=8, p2=32, ocv_compat=compat)
     e = oracle.effective(p, w, h)
     pix = np_bt_cost(left, right, minD, D, e["ftzero"])
-    ref = np_box_cost(pix, e["SW2"], e["SH2"], e["P2"], mode == 1)
+    ref = np_box_cost(pix, e["SW2"], e["SH2"], e["P2"], mode == 1, bool(compat & 1))
     got = oracle.ocv_cost(p, left, right)
     assert np.array_equal(got.astype(np.int64), ref)
 

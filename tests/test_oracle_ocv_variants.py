@@ -3,8 +3,10 @@ semantics targets"). The reference pins OpenCV only by ROS distro (melodic -> 3.
 noetic -> 4.2.0; .github/workflows/ros-build.yml:14-21, CMakeLists.txt:48-51) and OpenCV is
 absent here, so each divergence between versions / between computeDisparitySGBM's scalar
 and CV_SIMD branches is a switch of the restatement. Each test shows that the two
-behaviours differ on a constructed input and where they agree; the default (0) is the one
-the GPU engine reproduces bit-exactly (every GPU parity test).
+behaviours differ on a constructed input and where they agree. The bits come from
+`sgm_params.ocv_compat` (default COMPAT_MELODIC, the reference's Dockerfile build) OR-ed with the
+process-wide switch these KATs use; the GPU engine reproduces every combination bit-exactly
+(tests/test_gpu_ocv_compat.py).
 """
 import numpy as np
 import pytest
@@ -20,7 +22,7 @@ def _pair(synth, h, w, minD, D, seed):
 def _ocv(oracle, mode, **kw):
     m = oracle.MODE_OCV_SGBM5 if mode == "sgbm" else oracle.MODE_OCV_HH8
     base = dict(min_disparity=0, num_disparities=32, block_size=5, p1=8, p2=64, uniqueness_ratio=10,
-                prefilter_cap=31, speckle_window_size=0, speckle_range=0)
+                prefilter_cap=31, speckle_window_size=0, speckle_range=0, ocv_compat=0)
     base.update(kw)
     return oracle.make_params(m, **base)
 
@@ -125,8 +127,10 @@ def test_lane_tie_rule_changes_a_match(oracle):
 
 
 def test_default_is_the_engine_restatement(oracle, synth):
-    """The switches are off by default (the GPU engine's bit-exact target) and restored by
-    the context manager."""
+    """The process-wide switch is off by default (the parameter block decides) and restored by
+    the context manager; the parameter default is the melodic build."""
+    assert oracle.make_params(oracle.MODE_OCV_SGBM5).ocv_compat == oracle.COMPAT_MELODIC == 7
+    assert oracle.make_params(oracle.MODE_CENSUS8).ocv_compat == 0
     assert oracle.lib().sgmref_get_ocv_compat() == 0
     with oracle.ocv_compat(7):
         assert oracle.lib().sgmref_get_ocv_compat() == 7
