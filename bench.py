@@ -101,6 +101,18 @@ def cpu_baseline(cfg, budget_s=20.0):
     left, right, _ = synth.stereo_pair(cfg["h"], cfg["w"], 0, cfg["D"], seed=12345, with_truth=False)
     p = orc.make_params(orc.MODE_CENSUS8, num_disparities=cfg["D"], subpixel=cfg["subpixel"],
                         lr_check=cfg["lr_check"])
+    # cores: the CPUs this process may run on (affinity) and the cgroup quota, against the
+    # threads the port actually uses (OMP_NUM_THREADS: the GPU box's per-GPU CPU share is 16)
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
+    threads = max(1, min(threads, affinity, int(quota) if quota else affinity))
+    orc.set_threads(threads)
     threads = orc.num_threads()
     cpu_model = ""
     try:
@@ -115,7 +127,8 @@ def cpu_baseline(cfg, budget_s=20.0):
             break
     dt = time.perf_counter() - t0
     out = {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port", "cpu_model": cpu_model,
-           "host_cpus_visible": os.cpu_count(),
+           "host_cpus_visible": os.cpu_count(), "host_cpus_affinity": affinity, "cgroup_cpu_quota": quota,
+           "threads_used": threads,
            "sample": f"{n} full {cfg['w']}x{cfg['h']} D={cfg['D']} frames of the same census-SGM workload, "
                      f"oracle/sgm_oracle.c (OpenMP over lines, {threads} threads)"}
     # the reference's own CPU path: OpenCV-SGBM restatement, single thread, same geometry
@@ -129,6 +142,17 @@ def cpu_baseline(cfg, budget_s=20.0):
     out["reference_path"] = {"value": 1.0 / dt1, "unit": "pairs/s", "cores": 1, "kind": "port",
                              "sample": f"1 frame {cfg['w']}x{cfg['h']} D={cfg['D']} OpenCV-StereoSGBM "
                                        f"MODE_SGBM restatement (block 5), single-threaded like OpenCV"}
+    # the 8-path MODE_HH restatement at 1920x1080 D=128, single thread
+    ph = orc.make_params(orc.MODE_OCV_HH8, min_disparity=0, num_disparities=128, block_size=5,
+                         speckle_window_size=0)
+    orc.set_threads(1)
+    t0 = time.perf_counter()
+    orc.match(ph, left, right)
+    dth = time.perf_counter() - t0
+    out["reference_path_hh"] = {"value": 1.0 / dth, "unit": "pairs/s", "cores": 1, "kind": "port",
+                                "ms_per_frame": round(dth * 1e3, 1),
+                                "sample": f"1 frame {cfg['w']}x{cfg['h']} D=128 OpenCV-StereoSGBM MODE_HH "
+                                          f"restatement (block 5), single-threaded"}
     out["c1_reference_matcher"] = c1_reference_matcher(orc, synth)
     orc.set_threads(threads)
     return out

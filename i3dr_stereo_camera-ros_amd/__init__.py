@@ -55,7 +55,7 @@ def ocv_compat_from_env(default=COMPAT_MELODIC):
 
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
-    "sgm_check_params", "sgm_match", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
+    "sgm_check_params", "sgm_match", "sgm_match_f32", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
     "sgm_match_tiled_exact", "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
@@ -115,6 +115,7 @@ def load_library(path=None):
     L.sgm_get_params.argtypes = [vp, P(SgmParams)]
     L.sgm_check_params.argtypes = [P(SgmParams), ci, ci]
     L.sgm_match.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz]
+    L.sgm_match_f32.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz]
     L.sgm_match_device.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, vp]
     L.sgm_match_device_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, vp]
     L.sgm_match_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, P(ci), ci]
@@ -233,6 +234,19 @@ class Engine:
         h, w = left.shape
         out = np.empty((h, w), np.int16)
         self._check(self.lib.sgm_match(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w))
+        return out
+
+    def match_f32(self, left, right, out=None):
+        """sgm_match_f32: float32 disparity (x16 fixed point, the CV_32FC1 the node's matcher
+        contract returns), converted on the device; `out` (float32 rows) is filled in place."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        h, w = left.shape
+        if out is None:
+            out = np.empty((h, w), np.float32)
+        if out.dtype != np.float32 or out.shape != (h, w) or out.strides[1] != 4 or out.strides[0] < 4 * w:
+            raise ValueError("out must be a float32 (h, w) row-strided array")
+        self._check(self.lib.sgm_match_f32(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), out.strides[0] // 4))
         return out
 
     def match_device(self, d_left, d_right, width, height, stride, d_out, out_stride, stream=None):
@@ -643,19 +657,20 @@ class MatcherHIPSGM:
             self._engine = Engine(self.device)
         return self._engine
 
-    def _run(self, params, a, b):
+    def _run(self, params, a, b, f32=False):
         eng = self._engine_for()
         eng.set_params(params)
-        return eng.match(a, b)
+        return eng.match_f32(a, b) if f32 else eng.match(a, b)
 
     def forwardMatch(self):
         try:
-            disp = self._run(self.params, self.left, self.right)
             if self.interpolate:
-                # Q3: the WLS output is discarded and disparity_rl replaces disparity_lr
+                # Q3: the WLS output is discarded and disparity_rl (CV_16S) replaces disparity_lr
                 self.backwardMatch()
-                disp = self.disparity_rl
-            self.disparity_lr = disp.astype(np.float32)
+                self.disparity_lr = self.disparity_rl.astype(np.float32)
+            else:
+                # CV_32FC1 converted on the device (sgm_match_f32)
+                self.disparity_lr = self._run(self.params, self.left, self.right, f32=True)
             return 0
         except Exception as e:  # mirrors the catch(cv::Exception&) -> -1
             sys.stderr.write("Error in HIP SGM parameters\n%s\n" % e)

@@ -251,4 +251,19 @@ hipError_t launch_fill16(int16_t* d, size_t stride, int W, int H, int v, hipStre
     return hipGetLastError();
 }
 
+// disparity_lr.convertTo(CV_32FC1) on the device (abstractStereoMatcher.cpp:49, matcherOpenCVSGBM.cpp:34):
+// exact, every int16 is a float. Row strides in elements.
+__global__ __launch_bounds__(256) void k_to_f32(const int16_t* __restrict__ s, size_t ss, float* __restrict__ d, size_t ds,
+                                                int W)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x < W) d[(size_t)y * ds + x] = (float)s[(size_t)y * ss + x];
+}
+
+hipError_t launch_to_f32(const int16_t* s, size_t ss, float* d, size_t ds, int W, int H, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_to_f32, dim3((W + 255) / 256, H), dim3(256), 0, st, s, ss, d, ds, W);
+    return hipGetLastError();
+}
+
 }  // namespace sgm

@@ -38,9 +38,13 @@ hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
+int census_band_plan(const Geom&, int*, uint16_t*);
+hipError_t launch_census_single(const PathFrames&, const WtaFrames&, size_t, const Geom&, const uint32_t*, int, size_t,
+                                const Bands&, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
+hipError_t launch_to_f32(const int16_t*, size_t, float*, size_t, int, int, hipStream_t);
 hipError_t launch_disp_to_msg(const int16_t*, size_t, int, int, float, float, float*, size_t, hipStream_t);
 hipError_t launch_depth_points(const float*, size_t, int, int, const float*, double, double, const uint8_t*, size_t,
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
@@ -161,6 +165,7 @@ struct sgm_handle {
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
     std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
+    std::string bands_key;         // the same for the band plan of the gated single frame
     int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
     bool rect_on = false;          // sgm_set_rectification: batch inputs are raw, rectified in the census
     sgm::RectifyIn rect{};
@@ -255,8 +260,9 @@ int stage_index(sgm_handle* h, const char* name, double bytes)
 int ensure_ws(sgm_handle* h, size_t bytes)
 {
     if (h->ws.size >= bytes) return SGM_OK;
-    h->items_key[0].clear();       // contents (the path work lists) do not survive
+    h->items_key[0].clear();       // contents (the path work lists, the band plan) do not survive
     h->items_key[1].clear();
+    h->bands_key.clear();
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
         if (h->done_stream) (void)hipEventSynchronize(h->done);
@@ -309,9 +315,10 @@ struct Layout {
     int group = 1;                                         // frames per pipelined launch
     bool up_wta = false;                                   // pipelined batch: up+WTA scheme
     size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
+    size_t bands = 0; int n_bands = 0;                     // gated single frame: cnt | expect | order
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
-    size_t inL = 0, inR = 0, out = 0;                      // host-API staging
+    size_t inL = 0, inR = 0, out = 0, outf = 0;            // host-API staging (int16 / float out)
     size_t total = 0;
 };
 
@@ -352,6 +359,8 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         if (g.width1 > 0) {
             l.n_items[0] = sgm::census_path_items(g, 0xFFu, 1, 1, nullptr, 0);
             l.items[0] = take((size_t)l.n_items[0] * 4);
+            l.n_bands = sgm::census_band_plan(g, nullptr, nullptr);
+            l.bands = take((size_t)l.n_bands * 8 + (size_t)g.H * 2);
             if (group > 0) {
                 l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0, l.up_wta ? l.group : 0);
                 l.items[1] = take((size_t)l.n_items[1] * 4);
@@ -370,7 +379,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     }
     l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
-    if (host_io) { l.inL = take(WH); l.inR = take(WH); l.out = take(WH * 2); }
+    if (host_io) { l.inL = take(WH); l.inR = take(WH); l.out = take(WH * 2); l.outf = take(WH * 4); }
     l.total = off;
     return l;
 }
@@ -426,6 +435,35 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask,
     HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
     h->items_key[w] = key;
     return n;
+}
+
+// The band-gated single census frame (census_sgm.hip k_census_single16: the frame's WTA rows
+// in its paths launch, each row waiting for its band): on unless SGM_GATED=0, for volumes
+// whose sc1 stores fit 32-bit buffer offsets.
+bool use_gated(const Geom& g, const Layout& l)
+{
+    static const bool on = !std::getenv("SGM_GATED") || std::atoi(std::getenv("SGM_GATED")) != 0;
+    return on && g.width1 > 0 && l.n_bands > 0 && g.H < 65536 && (size_t)g.width1 * g.H * g.D < ((size_t)1 << 31);
+}
+
+// Device copy of the band plan (expect, order) for g, uploaded on `st` when the geometry or
+// the workspace changed; returns the Bands of the workspace (cnt not cleared).
+int band_plan(sgm_handle* h, const Layout& l, const Geom& g, hipStream_t st, sgm::Bands& bd)
+{
+    char* base = (char*)h->ws.base + l.bands;
+    bd.cnt = (int*)base;
+    bd.expect = (const int*)(base + (size_t)4 * l.n_bands);
+    bd.order = (const uint16_t*)(base + (size_t)8 * l.n_bands);
+    char key[160];
+    snprintf(key, sizeof key, "%d %d %d %d %p", g.W, g.H, g.D, g.minD, (void*)base);
+    if (h->bands_key == key) return SGM_OK;
+    std::vector<char> host((size_t)8 * l.n_bands + (size_t)2 * g.H);
+    sgm::census_band_plan(g, (int*)(host.data() + (size_t)4 * l.n_bands), (uint16_t*)(host.data() + (size_t)8 * l.n_bands));
+    HIP_TRY(hipMemcpyAsync(base + (size_t)4 * l.n_bands, host.data() + (size_t)4 * l.n_bands, host.size() - 4 * l.n_bands,
+                           hipMemcpyHostToDevice, st), "H2D band plan");
+    HIP_TRY(hipStreamSynchronize(st), "sync");    // rare (geometry changes): the host copy dies here
+    h->bands_key = key;
+    return SGM_OK;
 }
 
 // Post filters of one finished frame (src = the WTA output in `tmp` when a median runs).
@@ -485,10 +523,19 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
         sgm::WtaFrames wf{};
         wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
-        rec.begin("paths8", 8 * cells);
-        HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
-        rec.begin("wta_lr", 8 * cells + 2 * WH);
-        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
+        if (use_gated(g, l)) {       // one launch: the WTA rows wait for their bands
+            sgm::Bands bd;
+            int rc = band_plan(h, l, g, st, bd);
+            if (rc) return rc;
+            HIP_TRY(hipMemsetAsync(bd.cnt, 0, sizeof(int) * l.n_bands, st), "hipMemsetAsync");
+            rec.begin("paths8+wta_lr", 16 * cells + 2 * WH);
+            HIP_TRY(sgm::launch_census_single(pf, wf, l.vol_bytes, g, items, n_items, dst_stride, bd, st), "single");
+        } else {
+            rec.begin("paths8", 8 * cells);
+            HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
+            rec.begin("wta_lr", 8 * cells + 2 * WH);
+            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
+        }
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -694,7 +741,7 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     if ((rc = ensure_stream(h))) return rc;
     l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
-    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
+    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); h->bands_key.clear(); }
     return ensure_ws(h, l.total);
 }
 
@@ -759,7 +806,52 @@ int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H,
         q->done_stream = q->stream;
         HIP_TRY(hipStreamWaitEvent(h->stream, q->done, 0), "hipStreamWaitEvent");
     }
+    // lanes whose workspaces take more than a quarter of the device are not kept past the call
+    // (a later call on h, or another handle, may need that memory): the call waits for them
+    if ((size_t)(S - 1) * l0.total > total_b / 4) {
+        for (int s = 1; s < S; s++) {
+            sgm_handle* q = h->par[s - 1];
+            HIP_TRY(hipStreamSynchronize(q->stream), "hipStreamSynchronize");
+            HIP_TRY(hipFree(q->ws.base), "hipFree lane workspace");
+            q->ws = Workspace{};
+            q->items_key[0].clear();
+            q->items_key[1].clear();
+        }
+    }
     return SGM_OK;
+}
+
+// Host images in, host disparity out (sgm_match: int16; sgm_match_f32: the CV_32FC1 the
+// node's matcher contract wants, converted on the device). The reference's path is
+// matcherOpenCVSGBM.cpp:17-44 (compute, then convertTo CV_32FC1), called per frame from
+// generate_disparity.cpp:334-368. Every copy is one 2-D DMA between the caller's (pageable)
+// rows and the workspace: measured on the MI355X box (tools/probe/host_copy.cpp,
+// profiles/r03_host_copy.txt), a pageable 1920x1080 H2D takes 58 us against 42 us of CPU
+// packing + 45 us of pinned DMA, and the 8.3 MB float D2H runs at the same 53 GB/s into
+// pageable or pinned memory — staging buffers would only add copies.
+int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, void* out,
+               size_t out_stride, bool f32)
+{
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, true, g, l);
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
+    hipStream_t st = h->stream;
+    const size_t es = f32 ? 4 : 2;
+    char* ws = (char*)h->ws.base;
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, st), "H2D L");
+    HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
+    int16_t* d16 = (int16_t*)(ws + l.out);
+    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
+    if (rc) return rc;
+    const void* dsrc = d16;
+    if (f32) {
+        HIP_TRY(sgm::launch_to_f32(d16, W, (float*)(ws + l.outf), W, W, H, st), "to_f32");
+        dsrc = ws + l.outf;
+    }
+    HIP_TRY(hipMemcpy2DAsync(out, out_stride * es, dsrc, W * es, W * es, H, hipMemcpyDeviceToHost, st), "D2H");
+    HIP_TRY(hipStreamSynchronize(st), "sync");
+    return mark_done(h, st);
 }
 
 }  // namespace
@@ -1067,28 +1159,18 @@ int sgm_match(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, s
     if (h->rect_on) return fail(h, SGM_ERR_UNSUPPORTED, "fused rectification applies to device-buffer matches");
     if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W)
         return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
-    Geom g;
-    Layout l;
-    int rc = prepare(h, W, H, true, g, l);
-    if (rc || (rc = order_after_last(h, h->stream))) return rc;
-    const size_t WH = (size_t)W * H;
-    if ((rc = ensure_pin(h, WH * 4))) return rc;
-    char* ws = (char*)h->ws.base;
-    // pack rows into pinned staging (one H2D copy per image)
-    for (int y = 0; y < H; y++) {
-        std::memcpy(h->pin + (size_t)y * W, L + (size_t)y * stride, W);
-        std::memcpy(h->pin + WH + (size_t)y * W, R + (size_t)y * stride, W);
-    }
-    HIP_TRY(hipMemcpyAsync(ws + l.inL, h->pin, WH, hipMemcpyHostToDevice, h->stream), "H2D L");
-    HIP_TRY(hipMemcpyAsync(ws + l.inR, h->pin + WH, WH, hipMemcpyHostToDevice, h->stream), "H2D R");
-    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W,
-                      (int16_t*)(ws + l.out), W);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(h->pin, ws + l.out, WH * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
-    HIP_TRY(hipStreamSynchronize(h->stream), "sync");
-    const int16_t* src = (const int16_t*)h->pin;
-    for (int y = 0; y < H; y++) std::memcpy(disp + (size_t)y * out_stride, src + (size_t)y * W, 2 * (size_t)W);
-    return SGM_OK;
+    return match_host(h, L, R, W, H, stride, disp, out_stride, false);
+}
+
+int sgm_match_f32(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, float* disp,
+                  size_t out_stride)
+{
+    if (!h) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->rect_on) return fail(h, SGM_ERR_UNSUPPORTED, "fused rectification applies to device-buffer matches");
+    if (!L || !R || !disp || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W)
+        return fail(h, SGM_ERR_ARG, "bad buffers or sizes");
+    return match_host(h, L, R, W, H, stride, disp, out_stride, true);
 }
 
 }  // extern "C"

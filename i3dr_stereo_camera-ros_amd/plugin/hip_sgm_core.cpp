@@ -65,25 +65,21 @@ sgm_params MatcherCore::rightMatcherParams(const sgm_params& p)
     return r;
 }
 
-int MatcherCore::run(const sgm_params& p, const uint8_t* a, const uint8_t* b, int w, int h, size_t stride, float* out,
-                     size_t out_stride)
+// One host-buffer match: float32 output (the CV_32FC1 of matcherOpenCVSGBM.cpp:34, converted
+// on the device by sgm_match_f32) or int16 (CV_16S, the right matcher's disparity_rl).
+int MatcherCore::run(const sgm_params& p, const uint8_t* a, const uint8_t* b, int w, int h, size_t stride, float* outf,
+                     int16_t* out16, size_t out_stride)
 {
     int rc = SGM_OK;
     if (!handle_) rc = sgm_create(&handle_, device_);
     if (rc == SGM_OK) rc = sgm_set_params(handle_, &p);
-    if (rc == SGM_OK) {
-        buf_.resize((size_t)w * h);
-        rc = sgm_match(handle_, a, b, w, h, stride, buf_.data(), (size_t)w);
-    }
+    if (rc == SGM_OK)
+        rc = outf ? sgm_match_f32(handle_, a, b, w, h, stride, outf, out_stride)
+                  : sgm_match(handle_, a, b, w, h, stride, out16, out_stride);
     if (rc != SGM_OK) {
         err_ = handle_ ? sgm_last_error(handle_) : "no HIP device";
         std::cerr << "Error in HIP SGM parameters" << std::endl << err_ << " (status " << rc << ")" << std::endl;
         return -1;
-    }
-    for (int y = 0; y < h; y++) {
-        const int16_t* s = buf_.data() + (size_t)y * w;
-        float* d = out + (size_t)y * out_stride;
-        for (int x = 0; x < w; x++) d[x] = (float)s[x];   // convertTo(CV_32FC1): exact
     }
     return 0;
 }
@@ -93,13 +89,19 @@ int MatcherCore::forwardMatch(const uint8_t* left, const uint8_t* right, int w, 
 {
     if (interpolate_)  // Q3: WLS output discarded, right-view disparity returned
         return backwardMatch(left, right, w, h, stride, out, out_stride);
-    return run(params_, left, right, w, h, stride, out, out_stride);
+    return run(params_, left, right, w, h, stride, out, nullptr, out_stride);
 }
 
 int MatcherCore::backwardMatch(const uint8_t* left, const uint8_t* right, int w, int h, size_t stride, float* out,
                                size_t out_stride)
 {
-    return run(rightMatcherParams(params_), right, left, w, h, stride, out, out_stride);
+    return run(rightMatcherParams(params_), right, left, w, h, stride, out, nullptr, out_stride);
+}
+
+int MatcherCore::backwardMatch16(const uint8_t* left, const uint8_t* right, int w, int h, size_t stride, int16_t* out,
+                                 size_t out_stride)
+{
+    return run(rightMatcherParams(params_), right, left, w, h, stride, nullptr, out, out_stride);
 }
 
 }  // namespace sgm_hip

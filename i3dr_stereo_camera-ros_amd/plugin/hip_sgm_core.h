@@ -49,9 +49,12 @@ public:
     // catch(cv::Exception&) behaviour, matcherOpenCVSGBM.cpp:37-43).
     int forwardMatch(const uint8_t* left, const uint8_t* right, int width, int height, size_t stride,
                      float* out, size_t out_stride);
-    // right-view match (cv::ximgproc::createRightMatcher semantics) into `out`.
+    // right-view match (cv::ximgproc::createRightMatcher semantics) into `out`: float32, or
+    // int16 (backwardMatch16: the CV_16S disparity_rl of matcherOpenCVSGBM.cpp:46-51).
     int backwardMatch(const uint8_t* left, const uint8_t* right, int width, int height, size_t stride,
                       float* out, size_t out_stride);
+    int backwardMatch16(const uint8_t* left, const uint8_t* right, int width, int height, size_t stride,
+                        int16_t* out, size_t out_stride);
 
     const sgm_params& params() const { return params_; }
     bool interpolation() const { return interpolate_; }
@@ -60,13 +63,12 @@ public:
     static sgm_params rightMatcherParams(const sgm_params& p);
 
 private:
-    int run(const sgm_params& p, const uint8_t* a, const uint8_t* b, int w, int h, size_t stride, float* out,
-            size_t out_stride);
+    int run(const sgm_params& p, const uint8_t* a, const uint8_t* b, int w, int h, size_t stride, float* outf,
+            int16_t* out16, size_t out_stride);
     int device_;
     sgm_handle* handle_ = nullptr;   // opened lazily at the first match
     sgm_params params_{};
     bool interpolate_ = false;
-    std::vector<int16_t> buf_;
     std::string err_;
 };
 

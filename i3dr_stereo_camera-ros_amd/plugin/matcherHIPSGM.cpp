@@ -16,19 +16,27 @@ int MatcherHIPSGM::forwardMatch()
     std::cerr << "Error in HIP SGM parameters" << std::endl << "expects equal-size CV_8UC1 images" << std::endl;
     return -1;
   }
+  if (interpolate)
+  {
+    // Q3 (matcherOpenCVSGBM.cpp:22-33): the WLS output is discarded and the right-view
+    // disparity (CV_16S in disparity_rl) replaces disparity_lr
+    int rc = backwardMatch();
+    if (rc == 0)
+      disparity_rl.convertTo(disparity_lr, CV_32FC1);
+    return rc;
+  }
+  // CV_32FC1 straight from the device (matcherOpenCVSGBM.cpp:34's convertTo runs there)
   disparity_lr.create(left->size(), CV_32FC1);
-  int rc = core_.forwardMatch(left->data, right->data, left->cols, left->rows, left->step,
-                              (float *)disparity_lr.data, disparity_lr.step / sizeof(float));
-  if (rc == 0 && interpolate)
-    disparity_lr.copyTo(disparity_rl);   // Q3: the interp result IS the right-view disparity
-  return rc;
+  return core_.forwardMatch(left->data, right->data, left->cols, left->rows, left->step,
+                            (float *)disparity_lr.data, disparity_lr.step / sizeof(float));
 }
 
 int MatcherHIPSGM::backwardMatch()
 {
-  disparity_rl.create(left->size(), CV_32FC1);
-  return core_.backwardMatch(left->data, right->data, left->cols, left->rows, left->step,
-                             (float *)disparity_rl.data, disparity_rl.step / sizeof(float));
+  // CV_16S like createRightMatcher(matcher)->compute(*right, *left, disparity_rl) (:46-51)
+  disparity_rl.create(left->size(), CV_16S);
+  return core_.backwardMatch16(left->data, right->data, left->cols, left->rows, left->step,
+                               (int16_t *)disparity_rl.data, disparity_rl.step / sizeof(int16_t));
 }
 
 void MatcherHIPSGM::setMinDisparity(int min_disparity)

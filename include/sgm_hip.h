@@ -121,6 +121,13 @@ int  sgm_match(sgm_handle* h, const uint8_t* left, const uint8_t* right,
                int width, int height, size_t stride,
                int16_t* disp, size_t out_stride);
 
+/* sgm_match with the CV_32FC1 output of the reference's matcher contract
+ * (matcherOpenCVSGBM.cpp:34 `disparity_lr.convertTo(disparity_lr, CV_32FC1)`, still x16 fixed
+ * point): the int16 -> float conversion runs on the device, so the caller's buffer is filled by
+ * the D2H itself (out_stride in floats). Host buffers; synchronous.                        */
+int  sgm_match_f32(sgm_handle* h, const uint8_t* left, const uint8_t* right,
+                   int width, int height, size_t stride, float* disp, size_t out_stride);
+
 /* Device buffers in/out (already resident in HBM), asynchronous on `stream` (hipStream_t,
  * NULL = the handle's own stream). The handle's device must own the buffers. Calls on one
  * handle share its workspace, so each call is ordered after the previous one whatever the

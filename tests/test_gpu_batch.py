@@ -98,3 +98,26 @@ def test_async_calls_on_two_streams(engine, pkg, synth):
         torch.cuda.synchronize()
         for i in range(2):
             assert np.array_equal(outs[i].cpu().numpy(), refs[i]), f"rep {rep} stream {i}"
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_match_f32_host_rows(engine, pkg, synth, mode):
+    """sgm_match_f32 (the adapter's CV_32FC1 path, converted on the device) equals sgm_match's
+    int16 as float, with row-strided host inputs and output (2-D DMAs, no staging)."""
+    h, w = 90, 300
+    left, right, _ = synth.stereo_pair(h, w, 0, 64, seed=31)
+    p = pkg.default_params(mode, min_disparity=0, num_disparities=64, block_size=5)
+    engine.set_params(p)
+    ref = engine.match(left, right)
+    big_l = np.zeros((h, w + 37), np.uint8)
+    big_r = np.zeros((h, w + 37), np.uint8)
+    big_l[:, 5:5 + w] = left
+    big_r[:, 5:5 + w] = right
+    out = np.full((h, w + 11), -1.0, np.float32)
+    lib = pkg.load_library()
+    rc = lib.sgm_match_f32(engine.h, pkg._ptr(big_l[:, 5:]), pkg._ptr(big_r[:, 5:]), w, h, w + 37,
+                           pkg._ptr(out), w + 11)
+    assert rc == 0, engine.error()
+    assert np.array_equal(out[:, :w], ref.astype(np.float32))
+    assert (out[:, w:] == -1.0).all()                     # nothing written past the row
+    assert np.array_equal(engine.match_f32(left, right), ref.astype(np.float32))
