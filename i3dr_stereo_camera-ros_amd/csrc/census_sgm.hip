@@ -120,14 +120,11 @@ __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 
 }
 
 // the same from a raw buffer (base wave-uniform, byte offset off per lane)
-// cache policy of the volume loads: nt (streamed once), or sc1 (kPolSc1: the band-gated
-// single frame, whose volumes are handed over inside the launch, census_single16)
-constexpr int kPolNt = SGM_NT_LOAD ? 2 : 0, kPolSc1 = 16;
-template <int DPL, int AUX = kPolNt>
+template <int DPL>
 __device__ __forceinline__ void wload_buf(const uint8_t* base, uint32_t off, uint32_t (&wd)[(DPL + 3) / 4])
 {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
-    constexpr int aux = AUX;
+    constexpr int aux = SGM_NT_LOAD ? 2 : 0;           // 2: nt (streamed once)
     if constexpr (DPL == 2) { wd[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, aux); }
     else if constexpr (DPL == 4) { wd[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, aux); }
     else if constexpr (DPL == 8) {
@@ -174,49 +171,6 @@ __device__ __forceinline__ void store_pairs(uint8_t* dst, uint8_t* dst_hi, const
             else *d = v;
         }
     }
-}
-
-// The same through a buffer descriptor with sc1 (write-through) stores: the band-gated single
-// frame hands its volumes to WTA rows of the same launch on other XCDs (census_single16).
-// Offsets at or past the descriptor's range (kDrop) are dropped by the hardware.
-constexpr uint32_t kDrop = 0x80000000u;
-template <int DPL>
-__device__ __forceinline__ void store_pairs_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t off_hi,
-                                                const uint32_t (&L)[DPL / 2])
-{
-    if constexpr (DPL == 2) {
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)__builtin_amdgcn_perm(0u, L[0], 0x0c0c0200u), rs, off, 0, kPolSc1);
-    } else if constexpr (DPL == 4) {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(L[1], L[0], 0x06040200u), rs, off, 0, kPolSc1);
-    } else if constexpr (DPL == 8) {
-        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-        const v2u v = {__builtin_amdgcn_perm(L[1], L[0], 0x06040200u), __builtin_amdgcn_perm(L[3], L[2], 0x06040200u)};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, kPolSc1);
-    } else {
-        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int q = 0; q < DPL / 16; q++) {
-            const v4u v = {__builtin_amdgcn_perm(L[8 * q + 1], L[8 * q + 0], 0x06040200u),
-                           __builtin_amdgcn_perm(L[8 * q + 3], L[8 * q + 2], 0x06040200u),
-                           __builtin_amdgcn_perm(L[8 * q + 5], L[8 * q + 4], 0x06040200u),
-                           __builtin_amdgcn_perm(L[8 * q + 7], L[8 * q + 6], 0x06040200u)};
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, q == 0 ? off : off_hi, 0, kPolSc1);
-        }
-    }
-}
-
-// Band-gated single frame (census_single16): the path blocks count every finished band of
-// kBandRows rows into cnt[band]; the frame's WTA rows, dispatched after every path block of
-// the same launch, wait until their band's count reaches expect[band] (census_band_plan). The
-// hand-off is the MI355X write-through form: sc1 volume stores, each storing wave's vmcnt
-// wait before its workgroup's signal, a relaxed agent-scope atomic add by one lane, an sc1
-// poll and sc1 loads on the WTA side (no L2 write-back / invalidate). Bands start on 256-B
-// boundaries (16 rows x width1 x D, D % 16 == 0), so no cache line spans two bands.
-constexpr int kSigLag = 16;    // a band is signalled 16 steps after its last store: >= 32 VMEM ops
-                               // issued since, so s_waitcnt vmcnt(24) retires its stores without a stall
-__device__ __forceinline__ void band_signal(int* c)
-{
-    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Path-cost arithmetic in the "biased f16" domain. A cost v in [0, 1024) is held as the u16
@@ -350,7 +304,6 @@ __device__ __forceinline__ T pick4(const T (&a)[kMaxGroup], int f)
 
 constexpr int kWG = 256;          // 4 waves
 constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
-static_assert(kBandRows == kRowsPerWG, "a horizontal block's rows form one band");
 
 // ---------------------------------------------------------------- horizontal scans ----
 // Scalar operands per step come from 16-step chunks held one value per lane (lane j of a
@@ -373,8 +326,7 @@ __device__ __forceinline__ HChunk16 hload16(const uint64_t* cLr, const uint64_t*
     return c;
 }
 
-// SIG: sc1 stores through one descriptor over the volume (< 2 GB), for the band hand-off
-template <int DPL, bool EXACT, int DX, bool PRIO = false, bool SIG = false>
+template <int DPL, bool EXACT, int DX, bool PRIO = false>
 __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                           uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
                                           int y0)
@@ -405,9 +357,6 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
     HChunk16 cur = hload16<DPL, DX>(cLr, cRr, g, 0, p);
     HChunk16 nxt = cur;
-    const __amdgpu_buffer_rsrc_t rsv =
-        __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, SIG ? (int)((uint32_t)g.H * g.width1 * g.D) : 0, 0x00020000);
-    const uint32_t rowoff = (uint32_t)((size_t)yc * g.width1 * g.D + p * DPL);
     for (int b = 0; b * U < n; b++) {
         if constexpr (PRIO) lr_prio(((n - b * U) * SGM_LRPRIO_HW) >> 6, g.H);   // a scan step ~0.58 row steps
         static_for<0, U>([&](auto tc) {
@@ -422,13 +371,8 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
                                  P1P1, P2P2, imask, Labs);
             const int x1 = DX > 0 ? i : n - 1 - i;
             const bool ok = lane_ok && i < n;
-            if constexpr (SIG) {
-                const uint32_t o = rowoff + (uint32_t)x1 * (uint32_t)g.D;
-                store_pairs_sc1<DPL>(rsv, ok ? o : kDrop, (ok && hi_ok) ? o + 16u : kDrop, Labs);
-            } else {
-                uint8_t* dst = ok ? rowbase + (size_t)x1 * g.D : tr;
-                store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
-            }
+            uint8_t* dst = ok ? rowbase + (size_t)x1 * g.D : tr;
+            store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
             if constexpr (DX > 0) {
                 constexpr int ph = ((DPL - 1 - t) % DPL + DPL) % DPL;
                 cr[ph] = row_shr1_u64(cr[ph], inj);
@@ -566,12 +510,10 @@ __host__ __device__ constexpr size_t upwta_lds_bytes() { return (size_t)8 * 2 * 
 
 // NL lines of direction dir starting at base column xb (DPL disparities per lane, LPL
 // lanes per line; lds: 2 * RowSeg<DPL, LPL>::BUF codes).
-// SIG: sc1 volume stores and the band signals of census_single16 (bd.cnt)
-template <int DPL, bool EXACT, int LPL, bool FUSE = false, bool PRIO = false, bool SIG = false>
+template <int DPL, bool EXACT, int LPL, bool FUSE = false, bool PRIO = false>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
-                                         int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{},
-                                         const Bands& bd = Bands{})
+                                         int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{})
 {
     static_assert(!FUSE || LPL == 16, "up+WTA blocks use 16 lanes per line (the WTA layout)");
     using RS = RowSeg<DPL, LPL>;
@@ -642,15 +584,6 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         wta_emask<DPL, EXACT>(p, g, emaskE, emaskO);
         vload(s0);
     }
-    // SIG: bands in this block's sweep order (rows go up for ry < 0); band `pend` is signalled
-    // at step `due`, kSigLag steps after its last step, then the next one is pending
-    const int bstep = ry > 0 ? 1 : -1;
-    auto band_of = [&](int st) { return (ry > 0 ? st : g.H - 1 - st) / kBandRows; };
-    auto band_end = [&](int b) { return min(ry > 0 ? b * kBandRows + kBandRows - 1 : g.H - 1 - b * kBandRows, s1 - 1); };
-    const int blast = band_of(s1 - 1);
-    int pend = band_of(s0);
-    int due = SIG ? band_end(pend) + kSigLag : 0x7FFFFFFF;
-    const uint32_t rowbytes = (uint32_t)g.width1 * (uint32_t)g.D;
     auto step = [&](int s, const uint64_t* bufc) {
         const int x = xb + j + rx * s;
         const bool valid = s < s1 && x >= g.minX1 && x < g.maxX1;
@@ -702,12 +635,6 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
             typedef unsigned int v2u __attribute__((ext_vector_type(2)));
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), rr,
                                                   (valid && p == 0) ? (uint32_t)x * 8u : 0x80000000u, 0, 2);
-        } else if constexpr (SIG) {
-            const bool ok = valid && lane_act;
-            uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;   // wave-uniform
-            const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc((void*)vrow, 0, (int)rowbytes, 0x00020000);
-            const uint32_t o = (uint32_t)((x - g.minX1) * g.D + p * DPL);
-            store_pairs_sc1<DPL>(rsv, ok ? o : kDrop, (ok && hi_ok) ? o + 16u : kDrop, Labs);
         } else {
             const bool ok = valid && lane_act && !((SGM_EXP & 2) && dir == 1);
             uint8_t* const vrow = V + (size_t)min(max(y, 0), g.H - 1) * g.width1 * g.D;
@@ -723,14 +650,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         seg_load<DPL, LPL>(Rfree, sa, g, rx, ry, xb, min(s + 4, s1 - 1));
         step(s, bcur);
         seg_store<DPL, LPL>(bnext, Rnext, tid);
-        const bool sig = SIG && s == due;                // uniform
-        if (sig) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");   // the band's stores have retired
         __syncthreads();
-        if (sig) {
-            if (tid == 0) band_signal(bd.cnt + pend);
-            if (pend == blast) due = 0x7FFFFFFF;
-            else { pend += bstep; due = band_end(pend) + kSigLag; }
-        }
     };
     for (int s = s0; s < s1; s += 4) {
         if constexpr (PRIO) lr_prio(s1 - s, g.H);
@@ -739,15 +659,6 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         body(s + 2, buf0, buf1, R3, R2);
         body(s + 3, buf1, buf0, R0, R3);
     }
-    if (SIG && due != 0x7FFFFFFF) {                      // bands still inside their lag: drain, then signal
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0)
-            for (int b = pend;; b += bstep) {
-                band_signal(bd.cnt + b);
-                if (b == blast) break;
-            }
-    }
 }
 
 // One work-list entry: the lines of one block of one direction of one frame (16 rows for
@@ -755,10 +666,9 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 template <int DPL>
 __host__ __device__ constexpr int rows_lds_codes() { return 2 * RowSeg<RowsCfg<DPL>::DPL, RowsCfg<DPL>::LPL>::BUF; }
 
-template <int DPL, bool EXACT, bool PRIO = false, bool SIG = false>
+template <int DPL, bool EXACT, bool PRIO = false>
 __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_bytes, size_t trash_off,
-                                              const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds,
-                                              const Bands& bd = Bands{})
+                                              const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
     using RC = RowsCfg<DPL>;
     const int dir = (int)(it >> 24);
@@ -769,18 +679,9 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     const uint64_t* cR = pick4(pf.cR, f);
     uint8_t* V = pick4(pf.vols, f) + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
-    if (dir >= 6) {
-        if (dir == 6) p16_horiz<DPL, EXACT, 1, PRIO, SIG>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-        else p16_horiz<DPL, EXACT, -1, PRIO, SIG>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-        if constexpr (SIG) {                 // the block's 16 rows are band lb
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) band_signal(bd.cnt + lb);
-        }
-    } else {
-        p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO, SIG>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl,
-                                                           lds, UpWta{}, bd);
-    }
+    if (dir == 6) p16_horiz<DPL, EXACT, 1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else if (dir == 7) p16_horiz<DPL, EXACT, -1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    else p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
 }
 
 // SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
@@ -912,9 +813,8 @@ __device__ __forceinline__ void wta_emask(int p, const Geom& g, uint32_t (&emask
     }
 }
 
-// One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes. AUX: the volume loads'
-// cache policy (kPolSc1 in the band-gated single frame).
-template <int DPL, bool EXACT, int AUX = kPolNt>
+// One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
+template <int DPL, bool EXACT>
 __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size_t vol_bytes, const Geom& g,
                                           int16_t* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
 {
@@ -937,18 +837,17 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     const int n = g.width1;
     const int nq = (n + 3) / 4;
     // pixel 4q + r: the group's base is wave-uniform, the lane keeps one offset. The last
-    // group's rows past the row end re-read the row's last pixel (results never stored): reads
-    // stay inside the row, so a band-gated WTA row never touches a band not yet handed over.
+    // group reads up to 3 pixels past the row (the next row, or the volume's trash slot
+    // after the last row); their results are never stored.
     // Buffer loads (one descriptor per volume from the wave-uniform group base, the lane's
     // offset in a VGPR): no per-lane 64-bit address arithmetic.
     const uint32_t loff = off0 + (uint32_t)(r * g.D);
     auto load = [&](int q, uint32_t (&v)[8][NWD]) {
         const uint8_t* rowq = vols + row0 + (size_t)(4 * q) * g.D;
-        const uint32_t lo = 4 * q + r < n ? loff : off0 + (uint32_t)((n - 1 - 4 * q) * g.D);
 #pragma unroll
         for (int vv = 0; vv < 8; vv++) {
             if ((SGM_EXP & 4) && vv == 1) { for (int j = 0; j < NWD; j++) v[vv][j] = 0; continue; }
-            wload_buf<DPL, AUX>(rowq + (size_t)vv * vol_bytes, lo, v[vv]);
+            wload_buf<DPL>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
         }
     };
     // S in u16 pairs (wta_pix16). The next pixel group's loads are summed at the end of an
@@ -1146,37 +1045,6 @@ __global__ __launch_bounds__(kWG) void k_census_rowfin(WtaFrames wf, Geom g, siz
     row_finish(g, threadIdx.x, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, pick4(wf.out, f) + (size_t)y * out_stride);
 }
 
-// One frame in one launch with its WTA overlapped (the single-frame path of
-// sgm_match_device): blocks [0, n_items) are the frame's path work list (SIG: sc1 stores +
-// band signals), blocks [n_items, n_items + H) its WTA rows in bd.order, each waiting for its
-// band. Every path block has a lower block id than every WTA block, so all path blocks are
-// dispatched before the first WTA row can hold a slot: a waiting row never keeps a path block
-// from running. The wait is bounded (~4 s of polling); a frame that hit it would be wrong, not
-// hung.
-template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? SGM_WPE32 : SGM_WPE)))
-void k_census_single16(PathFrames pf, WtaFrames wf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                       const uint32_t* __restrict__ items, int n_items, size_t out_stride, Bands bd)
-{
-    extern __shared__ uint64_t lds_dyn64[];
-    const int b = blockIdx.x;
-    if (b < n_items) {
-        paths_block16<DPL, EXACT, true, true>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64, bd);
-        return;
-    }
-    const int y = bd.order[b - n_items];
-    if (threadIdx.x == 0) {
-        int* c = bd.cnt + y / kBandRows;
-        const int want = bd.expect[y / kBandRows];
-        for (int it = 0; it < (1 << 22); it++) {
-            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __syncthreads();
-    wta_row16<DPL, EXACT, kPolSc1>(wf.vols[0], vol_bytes, g, wf.out[0], out_stride, y, (uint32_t*)lds_dyn64);
-}
-
 // ------------------------------------------------------------------------------------
 // host-side launchers
 // ------------------------------------------------------------------------------------
@@ -1261,76 +1129,6 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
         out[round * n_slots + ((round & 1) ? in_round - 1 - i : i)] = v[k].code;
     }
     return n;
-}
-
-// Band plan of the band-gated single frame (k_census_single16): expect[b] = the signals band
-// b receives (every row-sweep block whose steps cover a row of it, and the two horizontal
-// blocks of its 16 rows), order = the WTA rows, bands in expected completion order: the
-// downward and upward sweeps meet in the middle, so the middle bands finish first.
-int census_band_plan(const Geom& g, int* expect, uint16_t* order)
-{
-    const int nb = (g.H + kBandRows - 1) / kBandRows;
-    if (!expect) return nb;
-    for (int b = 0; b < nb; b++) expect[b] = 2;                 // dirs 6 and 7: one block per band
-    const PathLaunch16 pl = make_path_launch16(g);
-    const int NL = rows_lines(g.D);
-    for (int dir = 0; dir < 6; dir++) {
-        const int rx = dir_rx(dir), ry = dir_ry(dir);
-        const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
-        const int nblk = (hi - pl.xb_lo[dir] + NL - 1) / NL;
-        for (int k = 0; k < nblk; k++) {
-            const int xb = pl.xb_lo[dir] + k * NL;
-            int s0, s1;      // p16_rows' step range
-            if (rx == 0) { s0 = 0; s1 = g.H; }
-            else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (NL - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
-            else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + NL - g.minX1); }
-            if (s0 >= s1) continue;
-            const int ylo = ry > 0 ? s0 : g.H - s1, yhi = ry > 0 ? s1 - 1 : g.H - 1 - s0;
-            for (int b = ylo / kBandRows; b <= yhi / kBandRows; b++) expect[b]++;
-        }
-    }
-    int n = 0;
-    const int mid = (nb - 1) / 2;
-    for (int d = 0; d <= nb; d++)
-        for (int side = 0; side < 2; side++) {
-            const int b = side == 0 ? mid - d : mid + 1 + d;
-            if (b < 0 || b >= nb) continue;
-            for (int y = b * kBandRows; y < std::min(g.H, (b + 1) * kBandRows); y++) order[n++] = (uint16_t)y;
-        }
-    return nb;
-}
-
-template <int DPL>
-static void launch_single_dpl(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, size_t trash_off,
-                              const Geom& g, const PathLaunch16& pl, const uint32_t* items, int n_items,
-                              size_t out_stride, const Bands& bd, hipStream_t st)
-{
-    const size_t lds = std::max(wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * rows_lds_codes<DPL>());
-    dim3 grid(n_items + g.H), block(kWG);
-    if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_single16<DPL, true>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride, bd);
-    else
-        hipLaunchKernelGGL((k_census_single16<DPL, false>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride, bd);
-}
-
-// The band-gated single frame: paths of pf's frame and WTA of wf's frame (the same frame) in
-// one launch; bd.cnt must be zero. Needs H < 65536 and a volume below 2 GB (sc1 stores through
-// 32-bit buffer offsets); the caller checks.
-hipError_t launch_census_single(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, const Geom& g,
-                                const uint32_t* items, int n_items, size_t out_stride, const Bands& bd, hipStream_t st)
-{
-    const PathLaunch16 pl = make_path_launch16(g);
-    const size_t trash_off = (size_t)g.H * g.width1 * g.D;
-    switch (dpl16_for(g.D)) {
-    case 2: launch_single_dpl<2>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 4: launch_single_dpl<4>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 8: launch_single_dpl<8>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 16: launch_single_dpl<16>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    default: launch_single_dpl<32>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    }
-    return hipGetLastError();
 }
 
 // SGM_TRACE=<file>: debug timeline of path / fused launches (one record per wave), written

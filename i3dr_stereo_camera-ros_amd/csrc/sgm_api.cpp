@@ -38,9 +38,6 @@ hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
-int census_band_plan(const Geom&, int*, uint16_t*);
-hipError_t launch_census_single(const PathFrames&, const WtaFrames&, size_t, const Geom&, const uint32_t*, int, size_t,
-                                const Bands&, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -165,7 +162,6 @@ struct sgm_handle {
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
     std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
-    std::string bands_key;         // the same for the band plan of the gated single frame
     int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
     bool rect_on = false;          // sgm_set_rectification: batch inputs are raw, rectified in the census
     sgm::RectifyIn rect{};
@@ -260,9 +256,8 @@ int stage_index(sgm_handle* h, const char* name, double bytes)
 int ensure_ws(sgm_handle* h, size_t bytes)
 {
     if (h->ws.size >= bytes) return SGM_OK;
-    h->items_key[0].clear();       // contents (the path work lists, the band plan) do not survive
+    h->items_key[0].clear();       // contents (the path work lists) do not survive
     h->items_key[1].clear();
-    h->bands_key.clear();
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
         if (h->done_stream) (void)hipEventSynchronize(h->done);
@@ -315,7 +310,6 @@ struct Layout {
     int group = 1;                                         // frames per pipelined launch
     bool up_wta = false;                                   // pipelined batch: up+WTA scheme
     size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
-    size_t bands = 0; int n_bands = 0;                     // gated single frame: cnt | expect | order
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0, outf = 0;            // host-API staging (int16 / float out)
@@ -359,8 +353,6 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         if (g.width1 > 0) {
             l.n_items[0] = sgm::census_path_items(g, 0xFFu, 1, 1, nullptr, 0);
             l.items[0] = take((size_t)l.n_items[0] * 4);
-            l.n_bands = sgm::census_band_plan(g, nullptr, nullptr);
-            l.bands = take((size_t)l.n_bands * 8 + (size_t)g.H * 2);
             if (group > 0) {
                 l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0, l.up_wta ? l.group : 0);
                 l.items[1] = take((size_t)l.n_items[1] * 4);
@@ -437,35 +429,6 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask,
     return n;
 }
 
-// The band-gated single census frame (census_sgm.hip k_census_single16: the frame's WTA rows
-// in its paths launch, each row waiting for its band): on unless SGM_GATED=0, for volumes
-// whose sc1 stores fit 32-bit buffer offsets.
-bool use_gated(const Geom& g, const Layout& l)
-{
-    static const bool on = !std::getenv("SGM_GATED") || std::atoi(std::getenv("SGM_GATED")) != 0;
-    return on && g.width1 > 0 && l.n_bands > 0 && g.H < 65536 && (size_t)g.width1 * g.H * g.D < ((size_t)1 << 31);
-}
-
-// Device copy of the band plan (expect, order) for g, uploaded on `st` when the geometry or
-// the workspace changed; returns the Bands of the workspace (cnt not cleared).
-int band_plan(sgm_handle* h, const Layout& l, const Geom& g, hipStream_t st, sgm::Bands& bd)
-{
-    char* base = (char*)h->ws.base + l.bands;
-    bd.cnt = (int*)base;
-    bd.expect = (const int*)(base + (size_t)4 * l.n_bands);
-    bd.order = (const uint16_t*)(base + (size_t)8 * l.n_bands);
-    char key[160];
-    snprintf(key, sizeof key, "%d %d %d %d %p", g.W, g.H, g.D, g.minD, (void*)base);
-    if (h->bands_key == key) return SGM_OK;
-    std::vector<char> host((size_t)8 * l.n_bands + (size_t)2 * g.H);
-    sgm::census_band_plan(g, (int*)(host.data() + (size_t)4 * l.n_bands), (uint16_t*)(host.data() + (size_t)8 * l.n_bands));
-    HIP_TRY(hipMemcpyAsync(base + (size_t)4 * l.n_bands, host.data() + (size_t)4 * l.n_bands, host.size() - 4 * l.n_bands,
-                           hipMemcpyHostToDevice, st), "H2D band plan");
-    HIP_TRY(hipStreamSynchronize(st), "sync");    // rare (geometry changes): the host copy dies here
-    h->bands_key = key;
-    return SGM_OK;
-}
-
 // Post filters of one finished frame (src = the WTA output in `tmp` when a median runs).
 // tmp_off: element offset of this frame's raw image in `tmp` (a pipelined group holds one
 // raw image per frame).
@@ -523,19 +486,10 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
         sgm::WtaFrames wf{};
         wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
-        if (use_gated(g, l)) {       // one launch: the WTA rows wait for their bands
-            sgm::Bands bd;
-            int rc = band_plan(h, l, g, st, bd);
-            if (rc) return rc;
-            HIP_TRY(hipMemsetAsync(bd.cnt, 0, sizeof(int) * l.n_bands, st), "hipMemsetAsync");
-            rec.begin("paths8+wta_lr", 16 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_single(pf, wf, l.vol_bytes, g, items, n_items, dst_stride, bd, st), "single");
-        } else {
-            rec.begin("paths8", 8 * cells);
-            HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
-            rec.begin("wta_lr", 8 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
-        }
+        rec.begin("paths8", 8 * cells);
+        HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
+        rec.begin("wta_lr", 8 * cells + 2 * WH);
+        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -741,7 +695,7 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     if ((rc = ensure_stream(h))) return rc;
     l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
-    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); h->bands_key.clear(); }
+    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
     return ensure_ws(h, l.total);
 }
 

@@ -290,14 +290,6 @@ struct WtaFrames {
     const uint64_t* cR[kMaxGroup];
     uint64_t* res[kMaxGroup];
 };
-// Band-gated single census frame (census_sgm.hip k_census_single16): signal counters, the
-// signals each band of kBandRows rows receives, and the WTA rows in dispatch order.
-struct Bands {
-    int* cnt;                 // [n_bands] signals, zeroed before the launch
-    const int* expect;        // [n_bands]
-    const uint16_t* order;    // [H]
-};
-constexpr int kBandRows = 16;
 // Rectification fused into the census: the census tile reads
 // remap(raw, map) instead of a rectified image. map[0..1] = left x/y, map[2..3] = right x/y,
 // each W x H of the rectified geometry; the raw images are src_w x src_h.

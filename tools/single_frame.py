@@ -1,8 +1,7 @@
 """Single-frame latency of the census engine (BASELINE configs[1] is one 1920x1080 D=128 frame;
 the node matches one frame per callback, generate_disparity.cpp:334-368): sgm_match_device on
 resident buffers, each call alone (stream synchronised before the next: what one callback
-sees), and back to back (HIP events over the reps). One JSON line per config; SGM_GATED=0 in
-the environment selects the two-launch path (paths8, then wta_lr) for an A/B.
+sees), and back to back (HIP events over the reps). One JSON line per config.
 
     python tools/single_frame.py [--reps 30] [--configs c2,c3]
 """
@@ -56,7 +55,7 @@ def main():
         e1.record(st)
         st.synchronize()
         eng.close()
-        print(json.dumps({"config": name, "W": W, "H": H, "D": D, "gated": os.environ.get("SGM_GATED", "1") != "0",
+        print(json.dumps({"config": name, "W": W, "H": H, "D": D,
                           "alone_ms_median": round(statistics.median(alone), 4), "alone_ms_min": round(min(alone), 4),
                           "back_to_back_ms": round(e0.elapsed_time(e1) / a.reps, 4),
                           "stages_ms": stages}), flush=True)
