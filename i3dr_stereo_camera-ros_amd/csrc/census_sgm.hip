@@ -51,39 +51,76 @@
 namespace sgm {
 
 // ------------------------------------------------------------------------------------
+// 9x7 census code of the pixel whose 9 x 7 window starts at byte tx of row ty of an LDS tile
+// (pitch a multiple of 4). Each window row is three aligned u32 reads and two alignbytes; the
+// 62 bits are produced from the highest down, each compare's result shifted into the code
+// (2 VALU per bit: byte compare, shift-add), instead of a u8 LDS read, compare, 64-bit shift
+// and or per bit. Bit order: LSB-first raster over the window, centre skipped.
+// ------------------------------------------------------------------------------------
+// acc = 2 * acc + (byte b of w < c): an SDWA byte compare into vcc and an add-with-carry
+// (b is a constant once the window loops are unrolled)
+#define SGM_CENSUS_BIT(B)                                                              \
+    asm("v_cmp_lt_u32_sdwa vcc, %1, %2 src0_sel:BYTE_" #B " src1_sel:DWORD\n\t"      \
+        "v_addc_co_u32_e32 %0, vcc, %0, %0, vcc"                                       \
+        : "+v"(acc) : "v"(w), "v"(c) : "vcc")
+__device__ __forceinline__ void census_bit(uint32_t& acc, uint32_t w, uint32_t c, int b)
+{
+    switch (b) {
+    case 0: SGM_CENSUS_BIT(0); break;
+    case 1: SGM_CENSUS_BIT(1); break;
+    case 2: SGM_CENSUS_BIT(2); break;
+    default: SGM_CENSUS_BIT(3); break;
+    }
+}
+#undef SGM_CENSUS_BIT
+
+template <int PITCH>
+__device__ __forceinline__ uint64_t census_code_lds(const uint8_t* tile, int ty, int tx)
+{
+    static_assert(PITCH % 4 == 0, "u32 rows");
+    const uint32_t* t32 = (const uint32_t*)tile + (PITCH / 4) * ty + (tx >> 2);
+    const int sb = tx & 3;
+    const uint32_t c = tile[(ty + 3) * PITCH + tx + 4];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int dy = 6; dy >= 0; dy--) {
+        const uint32_t* r = t32 + (PITCH / 4) * dy;
+        const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sb);   // window bytes 0..3
+        const uint32_t a1 = __builtin_amdgcn_alignbyte(w2, w1, sb);   // 4..7
+        const uint32_t a2 = __builtin_amdgcn_alignbyte(w2, w2, sb);   // 8 (low byte)
+#pragma unroll
+        for (int dx = 8; dx >= 0; dx--) {
+            if (dy == 3 && dx == 4) continue;
+            const int k = dy * 9 + dx - (dy * 9 + dx > 31 ? 1 : 0);    // bit index
+            const uint32_t w = dx < 4 ? a0 : dx < 8 ? a1 : a2;
+            if (k >= 32) census_bit(hi, w, c, dx & 3);
+            else census_bit(lo, w, c, dx & 3);
+        }
+    }
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 // 9x7 census: one thread per pixel, a 10 x 72 byte LDS tile per 64 x 4 pixel block.
 // blockIdx.z selects the image (0 = left, 1 = right).
-// ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_census9x7(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                    size_t stride, int W, int H,
                                                    uint64_t* __restrict__ cL, uint64_t* __restrict__ cR)
 {
-    __shared__ uint8_t tile[10][72];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[10 * 72];
     const uint8_t* img = blockIdx.z ? R : L;
     uint64_t* out = blockIdx.z ? cR : cL;
     const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 4;
     for (int i = threadIdx.x; i < 10 * 72; i += 256) {
         int ty = i / 72, tx = i - ty * 72;
         int yy = min(max(y0 + ty - 3, 0), H - 1), xx = min(max(x0 + tx - 4, 0), W - 1);
-        tile[ty][tx] = img[(size_t)yy * stride + xx];
+        tile[i] = img[(size_t)yy * stride + xx];
     }
     __syncthreads();
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int x = x0 + tx, y = y0 + ty;
     if (x >= W || y >= H) return;
-    const int c = tile[ty + 3][tx + 4];
-    uint64_t code = 0;
-    int bit = 0;
-#pragma unroll
-    for (int dy = 0; dy < 7; dy++) {
-#pragma unroll
-        for (int dx = 0; dx < 9; dx++) {
-            if (dy == 3 && dx == 4) continue;
-            code |= (uint64_t)(tile[ty + dy][tx + dx] < c) << bit;
-            bit++;
-        }
-    }
-    out[(size_t)y * W + x] = code;
+    out[(size_t)y * W + x] = census_code_lds<72>(tile, ty, tx);
 }
 
 // ====================================================================================
@@ -885,20 +922,22 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
-// block b: row b % H of frame b / H
+// block b: row y0 + b % ny of frame b / ny (rows [y0, y0 + ny) of every frame)
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void wta_block16(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride,
-                                            int b, uint32_t* lds)
+                                            int b, uint32_t* lds, int y0 = 0, int ny = 0)
 {
-    const int f = b / g.H;
-    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, b - f * g.H, lds);
+    if (ny <= 0) ny = g.H;
+    const int f = b / ny;
+    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, y0 + b - f * ny, lds);
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_bytes, Geom g, size_t out_stride)
+__global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_bytes, Geom g, size_t out_stride, int y0,
+                                                      int ny)
 {
     extern __shared__ uint32_t lds_dyn[];
-    wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn);
+    wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn, y0, ny);
 }
 
 // ------------------------------------------------------------------------------------
@@ -951,27 +990,14 @@ __device__ __forceinline__ void census_block(const CensusFrames& cf, int W, int 
     for (int ty = threadIdx.x >> 6; ty < kCensusRows; ty += kWG / 64) {
         const int y = y0 + ty;
         if (y >= H) break;
-        const uint8_t* t0 = tile + ty * 72 + tx;
-        const int c = t0[3 * 72 + 4];
-        uint64_t code = 0;
-        int bit = 0;
-#pragma unroll
-        for (int dy = 0; dy < 7; dy++) {
-#pragma unroll
-            for (int dx = 0; dx < 9; dx++) {
-                if (dy == 3 && dx == 4) continue;
-                code |= (uint64_t)(t0[dy * 72 + dx] < c) << bit;
-                bit++;
-            }
-        }
-        out[(size_t)y * W + x] = code;
+        out[(size_t)y * W + x] = census_code_lds<72>(tile, ty, tx);
     }
 }
 
 // census (optionally rectifying) of all frames of cf on its own: one block per 64 x 32 tile
 __global__ __launch_bounds__(kWG) void k_census_tiles(CensusFrames cf, int W, int H)
 {
-    __shared__ uint8_t tile[(kCensusRows + 6) * 72];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[(kCensusRows + 6) * 72];
     census_block(cf, W, H, blockIdx.x, tile);
 }
 
@@ -1205,25 +1231,30 @@ hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geo
 }
 
 template <int DPL>
-static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
+static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, int y0, int ny,
+                           hipStream_t st)
 {
-    dim3 grid(g.H * wf.n), block(kWG);
+    dim3 grid(ny * wf.n), block(kWG);
     const size_t lds = wta_lds_bytes<DPL>(g.W);
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
+        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride, y0, ny);
     else
-        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
+        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, wf, vol_bytes, g, out_stride, y0, ny);
 }
 
-// WTA + LR of the frames in wf (volumes -> disparity).
-hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
+// WTA + LR of rows [y0, y0 + ny) (ny < 0: to the last row) of the frames in wf (volumes ->
+// disparity). Rows are independent (disp2 and the LR check stay inside a row).
+hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st,
+                             int y0, int ny)
 {
+    if (ny < 0) ny = g.H - y0;
+    if (ny <= 0) return hipSuccess;
     switch (dpl16_for(g.D)) {
-    case 2: launch_wta_dpl<2>(wf, vol_bytes, g, out_stride, st); break;
-    case 4: launch_wta_dpl<4>(wf, vol_bytes, g, out_stride, st); break;
-    case 8: launch_wta_dpl<8>(wf, vol_bytes, g, out_stride, st); break;
-    case 16: launch_wta_dpl<16>(wf, vol_bytes, g, out_stride, st); break;
-    default: launch_wta_dpl<32>(wf, vol_bytes, g, out_stride, st); break;
+    case 2: launch_wta_dpl<2>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
+    case 4: launch_wta_dpl<4>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
+    case 8: launch_wta_dpl<8>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
+    case 16: launch_wta_dpl<16>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
+    default: launch_wta_dpl<32>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
     }
     return hipGetLastError();
 }
