@@ -36,6 +36,9 @@
 #ifndef SGM_LRPRIO_HW
 #define SGM_LRPRIO_HW 37   // a horizontal-scan step in row-sweep steps, x/64
 #endif
+#ifndef SGM_LRPRIO_DIAG
+#define SGM_LRPRIO_DIAG 64 // a diagonal row-sweep step in vertical row-sweep steps, x/64
+#endif
 #ifndef SGM_UPWTA_PRIO
 #define SGM_UPWTA_PRIO 0   // s_setprio of the up+WTA blocks (0: default priority)
 #endif
@@ -690,7 +693,7 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
         __syncthreads();
     };
     for (int s = s0; s < s1; s += 4) {
-        if constexpr (PRIO) lr_prio(s1 - s, g.H);
+        if constexpr (PRIO) lr_prio(rx != 0 ? ((s1 - s) * SGM_LRPRIO_DIAG) >> 6 : s1 - s, g.H);
         body(s, buf0, buf1, R1, R0);
         body(s + 1, buf1, buf0, R2, R1);
         body(s + 2, buf0, buf1, R3, R2);
@@ -922,22 +925,20 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
-// block b: row y0 + b % ny of frame b / ny (rows [y0, y0 + ny) of every frame)
+// block b: row b % H of frame b / H
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void wta_block16(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride,
-                                            int b, uint32_t* lds, int y0 = 0, int ny = 0)
+                                            int b, uint32_t* lds)
 {
-    if (ny <= 0) ny = g.H;
-    const int f = b / ny;
-    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, y0 + b - f * ny, lds);
+    const int f = b / g.H;
+    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, b - f * g.H, lds);
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_bytes, Geom g, size_t out_stride, int y0,
-                                                      int ny)
+__global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_bytes, Geom g, size_t out_stride)
 {
     extern __shared__ uint32_t lds_dyn[];
-    wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn, y0, ny);
+    wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1231,30 +1232,25 @@ hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geo
 }
 
 template <int DPL>
-static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, int y0, int ny,
-                           hipStream_t st)
+static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
 {
-    dim3 grid(ny * wf.n), block(kWG);
+    dim3 grid(g.H * wf.n), block(kWG);
     const size_t lds = wta_lds_bytes<DPL>(g.W);
     if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride, y0, ny);
+        hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
     else
-        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, wf, vol_bytes, g, out_stride, y0, ny);
+        hipLaunchKernelGGL((k_census_wta16<DPL, false>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
 }
 
-// WTA + LR of rows [y0, y0 + ny) (ny < 0: to the last row) of the frames in wf (volumes ->
-// disparity). Rows are independent (disp2 and the LR check stay inside a row).
-hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st,
-                             int y0, int ny)
+// WTA + LR of the frames in wf (volumes -> disparity).
+hipError_t launch_census_wta(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
 {
-    if (ny < 0) ny = g.H - y0;
-    if (ny <= 0) return hipSuccess;
     switch (dpl16_for(g.D)) {
-    case 2: launch_wta_dpl<2>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
-    case 4: launch_wta_dpl<4>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
-    case 8: launch_wta_dpl<8>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
-    case 16: launch_wta_dpl<16>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
-    default: launch_wta_dpl<32>(wf, vol_bytes, g, out_stride, y0, ny, st); break;
+    case 2: launch_wta_dpl<2>(wf, vol_bytes, g, out_stride, st); break;
+    case 4: launch_wta_dpl<4>(wf, vol_bytes, g, out_stride, st); break;
+    case 8: launch_wta_dpl<8>(wf, vol_bytes, g, out_stride, st); break;
+    case 16: launch_wta_dpl<16>(wf, vol_bytes, g, out_stride, st); break;
+    default: launch_wta_dpl<32>(wf, vol_bytes, g, out_stride, st); break;
     }
     return hipGetLastError();
 }

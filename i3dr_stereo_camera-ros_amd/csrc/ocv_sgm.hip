@@ -953,194 +953,6 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
     row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
-// ---- The two horizontal directions and the WTA in one pass over each row ----------------
-// OpenCV's MODE_SGBM runs its fifth path (x descending) in the same loop as the WTA; here
-// that stage takes both horizontal directions of a row. One wave per image row, lane p
-// holding d = p*DPL .. p*DPL + DPL - 1 (64 lanes, D <= 64 * DPL). The other directions arrive
-// as NV int16 volumes (slots 0..NV-1 of vols: MODE_SGBM dirs 0, 2, 3; MODE_HH dirs 0..5) from
-// k_ocv_paths. Below the overflow regime (not flagged) every path cost lies in [0, 32767]:
-// C' = P2 + SAD and L in [C' - P2, C'] (the recurrence's min term lies in [minLp, minLp + P2]),
-// so each of OpenCV's saturating sums, in whichever order, is min(sum, 32767):
-//   pass 1, x ascending:  L6 (dir 6), S1 = min(P + L6, 32767) -> s1 (int16 cells)
-//   pass 2, x descending: L7 (dir 7), S = min(S1 + L7, 32767), WTA of the pixel
-// then the shared disp2 / LR row epilogue. Bytes per cell: C' twice, the NV partial volumes
-// once, s1 written and read (2 + 2 NV + 2 + 4) against 2 + 2 + 2 for each horizontal direction
-// in k_ocv_paths + k_ocv_wta16.
-// Cells in flight per pass: a row is one wave's sequential walk, so each step's loads are
-// issued PF steps ahead to cover the HBM latency (~4 steps of the D = 480 step, ~16 of the
-// D <= 128 one), kept as packed int16 words.
-template <int DPL>
-__host__ __device__ constexpr int rows_pf() { return DPL <= 2 ? 16 : DPL == 4 ? 8 : 4; }
-template <int DPL>
-__device__ __forceinline__ void load_w16(const int16_t* p, uint32_t (&w)[(DPL + 1) / 2])
-{
-    if constexpr (DPL == 1) w[0] = (uint32_t)(uint16_t)*p;
-    else if constexpr (DPL == 2) w[0] = *(const uint32_t*)p;
-    else if constexpr (DPL == 4) { const uint2 t = *(const uint2*)p; w[0] = t.x; w[1] = t.y; }
-    else {
-#pragma unroll
-        for (int c = 0; c < DPL / 8; c++) {
-            const uint4 t = ((const uint4*)p)[c];
-            w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
-        }
-    }
-}
-template <int DPL>
-__device__ __forceinline__ int w16_at(const uint32_t (&w)[(DPL + 1) / 2], int k)
-{
-    return (k & 1) ? (int)w[k >> 1] >> 16 : (int)(int16_t)(uint16_t)w[k >> 1];
-}
-template <int DPL, int NV>
-__global__ __launch_bounds__(64) void k_ocv_rows(const int16_t* __restrict__ C, const int16_t* __restrict__ vols,
-                                                 size_t vol_elems, int16_t* __restrict__ s1, Geom g,
-                                                 int16_t* __restrict__ out, size_t out_stride)
-{
-    if (ocv_gate_skip<false>(g)) return;
-    constexpr int NW = (DPL + 1) / 2, PF = rows_pf<DPL>();
-    extern __shared__ uint32_t lds_rows[];
-    RowLds R(lds_rows, g.W);
-    const int lane = threadIdx.x, y = blockIdx.x;
-    R.init(g, lane, 64);
-    const bool lanetie = NV == 3 && (g.compat & SGM_OCV_LANE_TIE);   // MODE_SGBM's 3.x SSE2 ties
-    const int n = g.width1;
-    const bool lane_act = lane * DPL < g.D;
-    const int dl = lane_act ? lane * DPL : 0;      // lanes past D load group 0: never used for d < D
-    const size_t row0 = (size_t)y * n * g.D + dl;
-    const int16_t* Crow = C + row0;
-    const int16_t* Vrow = vols + row0;
-    int16_t* Srow = s1 + row0;
-    // ---- pass 1: dir 6 (x ascending), S1 = min(partial + L6, 32767)
-    {
-        uint32_t cb[PF][NW], vb[PF][NV][NW];
-        auto ld = [&](int q, int x) {
-            const size_t o = (size_t)min(x, n - 1) * g.D;
-            load_w16<DPL>(Crow + o, cb[q]);
-#pragma unroll
-            for (int v = 0; v < NV; v++) load_w16<DPL>(Vrow + (size_t)v * vol_elems + o, vb[q][v]);
-        };
-#pragma unroll
-        for (int q = 0; q < PF; q++) ld(q, q);
-        int Lp[DPL], mLp = 0;
-#pragma unroll
-        for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
-        for (int x0 = 0; x0 < n; x0 += PF) {
-#pragma unroll
-            for (int q = 0; q < PF; q++) {
-                const int x = x0 + q;
-                int Cp[DPL], P[DPL];
-#pragma unroll
-                for (int k = 0; k < DPL; k++) {
-                    Cp[k] = w16_at<DPL>(cb[q], k);
-                    int sum = 0;
-#pragma unroll
-                    for (int v = 0; v < NV; v++) sum += w16_at<DPL>(vb[q][v], k);
-                    P[k] = sum;
-                }
-                ld(q, x + PF);
-                if (x < n) {                        // uniform
-                    int L[DPL], Lraw[DPL], S1[DPL];
-                    const int lmin = ocv_step<DPL, 64, false>(Cp, Lp, mLp, x > 0, lane, g, L, Lraw);
-                    mLp = (int)(int16_t)line_min_i32<64>(lmin);
-#pragma unroll
-                    for (int k = 0; k < DPL; k++) {
-                        S1[k] = min(P[k] + L[k], kMaxCost);
-                        Lp[k] = L[k];
-                    }
-                    if (lane_act) store_i16<DPL>(Srow + (size_t)x * g.D, S1);   // idle lanes alias group 0
-                }
-            }
-        }
-    }
-    // ---- pass 2: dir 7 (x descending), S = min(S1 + L7, 32767), WTA
-    uint32_t cb[PF][NW], sb[PF][NW];
-    auto ld = [&](int q, int x) {
-        const size_t o = (size_t)max(x, 0) * g.D;
-        load_w16<DPL>(Crow + o, cb[q]);
-        load_w16<DPL>(Srow + o, sb[q]);
-    };
-#pragma unroll
-    for (int q = 0; q < PF; q++) ld(q, n - 1 - q);
-    int Lp[DPL], mLp = 0;
-#pragma unroll
-    for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
-    for (int i0 = 0; i0 < n; i0 += PF) {
-#pragma unroll
-        for (int q = 0; q < PF; q++) {
-            const int i = i0 + q, x1 = n - 1 - i;
-            int Cp[DPL], S[DPL];
-#pragma unroll
-            for (int k = 0; k < DPL; k++) { Cp[k] = w16_at<DPL>(cb[q], k); S[k] = w16_at<DPL>(sb[q], k); }
-            ld(q, x1 - PF);
-            if (i >= n) continue;                   // uniform
-            int L[DPL], Lraw[DPL];
-            const int lmin = ocv_step<DPL, 64, false>(Cp, Lp, mLp, i > 0, lane, g, L, Lraw);
-            mLp = (int)(int16_t)line_min_i32<64>(lmin);
-            int km = 0x7FFFFFFF;
-#pragma unroll
-            for (int k = 0; k < DPL; k++) {
-                Lp[k] = L[k];
-                S[k] = min(S[k] + L[k], kMaxCost);
-                const int d = lane * DPL + k;
-                const int key = (S[k] << 11) | wta_tie(d, lanetie, 11);
-                km = (lane_act && d < g.D) ? min(km, key) : km;
-            }
-            const int kmin = wave_min(km);
-            const int best = wta_untie(kmin & 2047, lanetie, 11), minS = kmin >> 11;
-            bool hit = false;
-            const int bm = max(best - 1, 0), bp = min(best + 1, g.D - 1);
-            int vm = 0, vp = 0;
-#pragma unroll
-            for (int k = 0; k < DPL; k++) {
-                const int d = lane * DPL + k;
-                hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
-                vm += d == bm ? S[k] : 0;
-                vp += d == bp ? S[k] : 0;
-            }
-            // every S saturated at MAX_COST: OpenCV's bestDisp stays -1 (see k_ocv_wta16)
-            const bool rej = __ballot(hit) != 0ull || minS >= kMaxCost;
-            const int sm = __builtin_amdgcn_readlane(vm, bm / DPL), sp = __builtin_amdgcn_readlane(vp, bp / DPL);
-            const int den = max(sm + sp - 2 * minS, 1);
-            const bool use = g.subpix && best > 0 && best < g.D - 1;
-            const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
-            if (lane == 0) {
-                const int x = g.minX1 + x1;
-                R.bst[x] = (int16_t)(rej ? -1 : best);
-                R.mins[x] = (uint16_t)minS;
-                if (!rej) R.drow[x] = (int16_t)d16;
-            }
-        }
-    }
-    row_finish(g, lane, 64, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
-}
-
-template <int DPL>
-static void launch_ocv_rows_dpl(const int16_t* C, const void* vols, size_t cells, int nv, int16_t* s1, const Geom& g,
-                                int16_t* out, size_t out_stride, hipStream_t st)
-{
-    const size_t ve = ocv_vol_elems(cells, 2);
-    const int16_t* v = (const int16_t*)vols;
-    const size_t lds = RowLds::bytes(g.W);
-    if (nv == 3)
-        hipLaunchKernelGGL((k_ocv_rows<DPL, 3>), dim3(g.H), dim3(64), lds, st, C, v, ve, s1, g, out, out_stride);
-    else
-        hipLaunchKernelGGL((k_ocv_rows<DPL, 6>), dim3(g.H), dim3(64), lds, st, C, v, ve, s1, g, out, out_stride);
-}
-
-// The OCV modes' horizontal pair + WTA (k_ocv_rows) over the plain (not flagged) frame: nv = 3
-// (MODE_SGBM) or 6 (MODE_HH) int16 volumes from k_ocv_paths; s1 = a cells-sized int16 scratch.
-bool ocv_rows_supported(const Geom& g) { return g.wide != 1 && g.D <= 1024 && g.width1 > 0; }
-hipError_t launch_ocv_rows(const int16_t* C, const void* vols, size_t cells, int nv, int16_t* s1, const Geom& g,
-                           int16_t* out, size_t out_stride, hipStream_t st)
-{
-    const int D = g.D;
-    if (D <= 64) launch_ocv_rows_dpl<1>(C, vols, cells, nv, s1, g, out, out_stride, st);
-    else if (D <= 128) launch_ocv_rows_dpl<2>(C, vols, cells, nv, s1, g, out, out_stride, st);
-    else if (D <= 256) launch_ocv_rows_dpl<4>(C, vols, cells, nv, s1, g, out, out_stride, st);
-    else if (D <= 512) launch_ocv_rows_dpl<8>(C, vols, cells, nv, s1, g, out, out_stride, st);
-    else launch_ocv_rows_dpl<16>(C, vols, cells, nv, s1, g, out, out_stride, st);
-    return hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------
 static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
@@ -1203,10 +1015,10 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
 // matching the frame's flag exits at once
 template <int DPL, int LPL>
 static void launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
-                               int dirmask, int kinds, hipStream_t st)
+                               int dirmask, hipStream_t st)
 {
-    if (g.wide != 1 && (kinds & 1)) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st);
-    if (g.wide == 0 || !(kinds & 2)) return;
+    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st);
+    if (g.wide == 0) return;
     if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st);
     else launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st);
 }
@@ -1232,27 +1044,26 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
     return waves < kOcvWideLineWaves ? 32 : 16;
 }
 
-// kinds: bit 0 the plain kernels, bit 1 the flagged ones (Geom::wide)
 hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
-                            int dirmask, hipStream_t st, int kinds)
+                            int dirmask, hipStream_t st)
 {
     const int D = g.D;
     const int lpl = ocv_lanes_per_line(g, dirmask);
     if (lpl == 64) {
-        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, kinds, st);
-        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, kinds, st);
+        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st);
     } else if (lpl == 32) {
-        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, kinds, st);
-        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, kinds, st);
-        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, kinds, st);
-        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, kinds, st);
+        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st);
+        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, kinds, st); break;
-        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, kinds, st); break;
-        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, kinds, st); break;
-        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, kinds, st); break;
-        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, kinds, st); break;   // D <= 256 here
+        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st); break;
+        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st); break;   // D <= 256 here
         }
     }
     return hipGetLastError();
@@ -1297,10 +1108,10 @@ static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geo
 // SIMD_SAT), or a region sized for the larger, read as the one the cost kernel's overflow
 // flag selects (wide 2); cells = width1 * H * D per volume
 hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
-                          size_t out_stride, hipStream_t st, int kinds)
+                          size_t out_stride, hipStream_t st)
 {
-    if (g.wide != 1 && (kinds & 1)) launch_ocv_wta_t<int16_t, false>(vols, cells, ndir, g, out, out_stride, st);
-    if (g.wide == 0 || !(kinds & 2)) return hipGetLastError();
+    if (g.wide != 1) launch_ocv_wta_t<int16_t, false>(vols, cells, ndir, g, out, out_stride, st);
+    if (g.wide == 0) return hipGetLastError();
     if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_wta_t<int16_t, true>(vols, cells, ndir, g, out, out_stride, st);
     else launch_ocv_wta_t<int32_t, false>(vols, cells, ndir, g, out, out_stride, st);
     return hipGetLastError();

@@ -27,7 +27,7 @@ hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint6
 int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int, int up_group = 0);
 hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t,
                                const uint8_t* = nullptr, const uint8_t* = nullptr, size_t = 0);
-hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t, int y0 = 0, int ny = -1);
+hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
 hipError_t launch_rectify_map(const double*, const double*, const double*, int, int, float*, float*, size_t,
                               hipStream_t);
 hipError_t launch_remap_cubic(const uint8_t*, size_t, int, int, const float*, const float*, size_t, int, int,
@@ -47,10 +47,8 @@ hipError_t launch_depth_points(const float*, size_t, int, int, const float*, dou
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
-hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t, int kinds = 3);
-hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t, int kinds = 3);
-bool ocv_rows_supported(const Geom&);
-hipError_t launch_ocv_rows(const int16_t*, const void*, size_t, int, int16_t*, const Geom&, int16_t*, size_t, hipStream_t);
+hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
 }  // namespace sgm
 
 using sgm::Geom;
@@ -130,8 +128,6 @@ int make_geom(const sgm_params& p, int W, int H, Geom& g, std::string& err)
 
 bool use_median(const sgm_params& p) { return p.mode != SGM_MODE_CENSUS8 || p.median != 0; }
 
-constexpr int kHostChunks = 4;     // WTA row chunks of a host-buffer call (copy-out overlap)
-
 struct Workspace {
     void* base = nullptr;
     size_t size = 0;
@@ -178,7 +174,6 @@ struct sgm_handle {
     hipEvent_t par_ev = nullptr;   // recorded on the handle's stream, then each lane's done
     hipStream_t stream2 = nullptr;
     hipEvent_t bev[4] = {};
-    hipEvent_t host_ev[4] = {};    // match_host: the WTA row chunks whose copy-out may start
     // cross-call ordering: every call that uses the workspace records `done` on the stream it
     // ran on, and the next call (whatever its stream) waits on it first
     hipEvent_t done = nullptr;
@@ -434,18 +429,6 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask,
     return n;
 }
 
-// OCV modes: the horizontal pair + WTA per row (k_ocv_rows) unless SGM_OCV_ROWS=0 (the
-// per-direction volumes + k_ocv_wta16 scheme, kept for A/B and for the cases it does not cover:
-// int32-only frames (wide == 1) and D > 1024)
-bool use_ocv_rows(const Geom& g)
-{
-    const char* e = std::getenv("SGM_OCV_ROWS");    // read per frame (A/B, tests); measured slower: off
-    return e && std::atoi(e) != 0 && sgm::ocv_rows_supported(g);
-}
-
-// first row of chunk k of n over H rows
-int chunk_row(int H, int n, int k) { return (int)((long long)H * k / n); }
-
 // Post filters of one finished frame (src = the WTA output in `tmp` when a median runs).
 // tmp_off: element offset of this frame's raw image in `tmp` (a pipelined group holds one
 // raw image per frame).
@@ -472,15 +455,9 @@ int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_
 }
 
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
-// n_chunks > 0 (host-buffer calls): when the census WTA writes the final disparities (no
-// median / speckle stage after it) it runs as n_chunks row ranges, chunk_ev[k] recorded after
-// chunk k, and *chunked = n_chunks, so the caller's copy-out of a finished range overlaps the
-// WTA of the next (rows are independent: disp2 and the LR check stay inside a row).
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
-                 int16_t* dOut, size_t out_stride, int n_chunks = 0, hipEvent_t* chunk_ev = nullptr,
-                 int* chunked = nullptr)
+                 int16_t* dOut, size_t out_stride)
 {
-    if (chunked) *chunked = 0;
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
     hipStream_t st = h->stream;
@@ -512,16 +489,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
-        if (n_chunks > 0 && chunk_ev && !med && p.speckle_window_size <= 0 && !h->profiling) {
-            for (int k = 0; k < n_chunks; k++) {
-                const int y0 = chunk_row(g.H, n_chunks, k), y1 = chunk_row(g.H, n_chunks, k + 1);
-                HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st, y0, y1 - y0), "wta");
-                HIP_TRY(hipEventRecord(chunk_ev[k], st), "hipEventRecord");
-            }
-            *chunked = n_chunks;
-        } else {
-            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
-        }
+        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -538,25 +506,10 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         const double es = g.wide == 1 && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // gated: the int16 case
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
         HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, gg, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
-        if (use_ocv_rows(gg)) {
-            // the vertical and diagonal directions as volumes, then both horizontal directions
-            // and the WTA per row (k_ocv_rows); frames the overflow flag marks (wide == 2) take
-            // the flagged kernels after them, each launch gated on the flag
-            const int nv = fullDP ? 6 : 3;
-            rec.begin("ocv_paths", (double)nv * 4 * cells);
-            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, fullDP ? 0x3F : 0x0D, st, 1), "ocv_paths");
-            rec.begin("ocv_rows_wta_lr", (2.0 * nv + 8) * cells + 2 * WH);
-            HIP_TRY(sgm::launch_ocv_rows(A, V, ncells, nv, B, gg, dst, dst_stride, st), "ocv_rows");
-            if (g.wide == 2) {
-                HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st, 2), "ocv_paths");
-                HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st, 2), "ocv_wta");
-            }
-        } else {
-            rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
-            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
-            rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
-            HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
-        }
+        rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
+        HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
+        rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
+        HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
     }
     int rc = run_post(h, l, g, dOut, out_stride, rec);
     if (rc) return rc;
@@ -843,37 +796,8 @@ int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, 
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, st), "H2D L");
     HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
     int16_t* d16 = (int16_t*)(ws + l.out);
-    // the copy-out overlaps the WTA: chunks of rows on the second stream as they finish
-    // (census mode without post filters; every WTA chunk is queued before the first copy,
-    // whose pageable destination may hold this thread until the data is there)
-    int nck = 0;
-    if (!h->stream2) HIP_TRY(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking), "hipStreamCreate");
-    for (hipEvent_t& e : h->host_ev)
-        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-    const char* ce = std::getenv("SGM_HOST_CHUNKS");      // A/B: 0 = one WTA launch, one copy
-    const int chunks = ce ? std::min(std::max(std::atoi(ce), 0), kHostChunks) : 0;   // measured no gain: off
-    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W, chunks,
-                      h->host_ev, &nck);
+    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
     if (rc) return rc;
-    if (nck > 0) {
-        hipStream_t s2 = h->stream2;
-        for (int k = 0; k < nck; k++) {
-            const int y0 = chunk_row(H, nck, k), ny = chunk_row(H, nck, k + 1) - y0;
-            HIP_TRY(hipStreamWaitEvent(s2, h->host_ev[k], 0), "hipStreamWaitEvent");
-            const void* src = d16 + (size_t)y0 * W;
-            if (f32) {
-                float* f = (float*)(ws + l.outf) + (size_t)y0 * W;
-                HIP_TRY(sgm::launch_to_f32(d16 + (size_t)y0 * W, W, f, W, W, ny, s2), "to_f32");
-                src = f;
-            }
-            HIP_TRY(hipMemcpy2DAsync((char*)out + (size_t)y0 * out_stride * es, out_stride * es, src, W * es, W * es, ny,
-                                     hipMemcpyDeviceToHost, s2),
-                    "D2H");
-        }
-        HIP_TRY(hipStreamSynchronize(s2), "sync");
-        HIP_TRY(hipStreamSynchronize(st), "sync");
-        return mark_done(h, st);
-    }
     const void* dsrc = d16;
     if (f32) {
         HIP_TRY(sgm::launch_to_f32(d16, W, (float*)(ws + l.outf), W, W, H, st), "to_f32");
@@ -939,7 +863,6 @@ void sgm_destroy(sgm_handle* h)
         if (h->stream2) (void)hipStreamSynchronize(h->stream2);
         if (h->done_stream) (void)hipEventSynchronize(h->done);   // the last call on a caller's stream
         for (hipEvent_t e : h->bev) if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : h->host_ev) if (e) (void)hipEventDestroy(e);
         if (h->stream2) (void)hipStreamDestroy(h->stream2);
         if (h->ws.base) (void)hipFree(h->ws.base);
         if (h->pin) (void)hipHostFree(h->pin);

@@ -89,27 +89,6 @@ def test_ocv_path_lanes_per_line(engine, oracle, synth, pkg, monkeypatch, nobuf,
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
-@COMPATS
-@pytest.mark.parametrize("rows", ["0", "1"], ids=["volumes", "rows"])
-@pytest.mark.parametrize("mode,h,w,minD,D,block", [(0, 480, 640, 9, 64, 15), (1, 96, 500, 0, 128, 5),
-                                                   (0, 40, 600, -4, 256, 7), (1, 33, 200, 3, 48, 3),
-                                                   (0, 24, 1400, -3, 480, 9), (1, 20, 1500, 147, 1024, 21),
-                                                   (0, 12, 80, 0, 16, 3), (1, 9, 70, 2, 64, 5),
-                                                   (0, 30, 300, 5, 112, 11)])
-def test_ocv_rows_schemes(engine, oracle, synth, pkg, monkeypatch, rows, mode, h, w, minD, D, block, compat):
-    """The OCV path stage's schemes (SGM_OCV_ROWS): every direction as a volume + the WTA rows
-    (0); the vertical / diagonal directions as volumes, then both horizontal directions and the
-    WTA in one pass per row (1, the default, k_ocv_rows). Widths shorter than the prefetch
-    depth, D from 16 to 1024 (64 lanes x 1..16 values), both build variants."""
-    monkeypatch.setenv("SGM_OCV_ROWS", rows)
-    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h + w + D)
-    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, ocv_compat=compat)
-    engine.set_params(p)
-    got = engine.match(left, right)
-    ref = oracle.match(to_oracle_params(oracle, p), left, right)
-    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
-
-
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("uniq", [0, 10])
 def test_ocv_saturated_sums(engine, oracle, pkg, mode, uniq):
