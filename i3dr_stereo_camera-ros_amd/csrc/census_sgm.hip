@@ -45,6 +45,9 @@
 #ifndef SGM_ROWS_LPL8
 #define SGM_ROWS_LPL8 0    // 1: row sweeps with 8 lanes per path line for D <= 256 (RowsCfg; measured slower)
 #endif
+#ifndef SGM_P32
+#define SGM_P32 1          // D > 256: 32-lane path lines of 16 disparities per lane (0: 16 lanes x 32, LineCfg)
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -280,17 +283,19 @@ __device__ __forceinline__ void p16_relative(const uint32_t (&Labs)[DPL / 2], ui
 // min reduction, 1 subtract.
 // LPL = 8: the line's lanes are every other lane of a 16-lane row, so the neighbouring lane
 // of the same line is 2 lanes away (row_shr:2 / row_shl:2; both lines' edge lanes read kInf).
+// LPL = 32: a line is a row pair; the neighbours cross the row boundary (line32_shr1/shl1).
 template <int DPL, bool EXACT, int LPL = 16, typename F>
 __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F crk, uint32_t P1P1, uint32_t P2P2,
                                          const uint32_t (&imask)[DPL / 2], uint32_t (&Labs)[DPL / 2])
 {
     constexpr int M = DPL / 2;
-    constexpr int SH = LPL == 16 ? 1 : 2;
+    constexpr int SH = LPL == 8 ? 2 : 1;
     uint32_t q[M];
 #pragma unroll
     for (int i = 0; i < M; i++) q[i] = Lr[i] + P1P1;      // = pk_add: halves <= kInfP | kBaseP, no carry
-    const uint32_t X = row_shr_n<SH>(q[M - 1], kInfP2);   // previous lane: its .hi is q(d0 - 1)
-    const uint32_t Y = row_shl_n<SH>(q[0], kInfP2);       // next lane: its .lo is q(d0 + DPL)
+    // previous lane: its .hi is q(d0 - 1); next lane: its .lo is q(d0 + DPL)
+    const uint32_t X = LPL == 32 ? line32_shr1(q[M - 1], kInfP2) : row_shr_n<SH>(q[M - 1], kInfP2);
+    const uint32_t Y = LPL == 32 ? line32_shl1(q[0], kInfP2) : row_shl_n<SH>(q[0], kInfP2);
     uint32_t Oprev = alignbit16(q[0], X);                 // (q(d-1), q(d)) for pair 0
 #pragma unroll
     for (int i = 0; i < M; i++) {
@@ -343,7 +348,18 @@ __device__ __forceinline__ T pick4(const T (&a)[kMaxGroup], int f)
 }
 
 constexpr int kWG = 256;          // 4 waves
-constexpr int kRowsPerWG = 16;    // horizontal scans: 4 rows per wave
+
+// Lanes per path line of a launch whose 16-lane layout would hold DPL16 disparities per lane.
+// D > 256 (DPL16 = 32) runs 32-lane lines of 16 disparities per lane: the 16-lane form's 32
+// values per lane held the kernel at 128 VGPRs (4 waves/SIMD) and made each step one long
+// dependent chain; 32-lane lines keep the D <= 256 register budget at the price of one
+// cross-row select per neighbour exchange and a permlane16 swap in the min over D.
+template <int DPL16>
+struct LineCfg {
+    static constexpr int LPL = (DPL16 == 32 && SGM_P32) ? 32 : 16;
+    static constexpr int DPL = DPL16 * 16 / LPL;       // disparities per lane
+    static constexpr int HROWS = 4 * (64 / LPL);       // image rows per horizontal-scan workgroup
+};
 
 // ---------------------------------------------------------------- horizontal scans ----
 // Scalar operands per step come from 16-step chunks held one value per lane (lane j of a
@@ -353,28 +369,34 @@ struct HChunk16 {
     uint64_t cl, inj;
 };
 
-template <int DPL, int DX>
+// entries of chunk `chunk` for the 16 lanes of a row (i16 = lane within the row); LPL: lanes
+// per line (the window spans LPL * DPL disparities)
+template <int DPL, int DX, int LPL>
 __device__ __forceinline__ HChunk16 hload16(const uint64_t* cLr, const uint64_t* cRr, const Geom& g, int chunk,
-                                            int p)
+                                            int i16)
 {
-    const int i = chunk * 16 + p;
+    const int i = chunk * 16 + i16;
     const int x = DX > 0 ? g.minX1 + i : g.maxX1 - 1 - i;
     HChunk16 c;
     c.cl = cLr[min(max(x, 0), g.W - 1)];
-    const int xr = DX > 0 ? x + 1 - g.minD : x - g.minD - 16 * DPL;   // code entering the window
+    const int xr = DX > 0 ? x + 1 - g.minD : x - g.minD - LPL * DPL;   // code entering the window
     c.inj = cRr[min(max(xr, 0), g.W - 1)];
     return c;
 }
 
-template <int DPL, bool EXACT, int DX, bool PRIO = false>
+// One image row per path line (LPL = 16: four lines per wave; 32: two, each a row pair of
+// lanes), rows y0 + line. With 32-lane lines both rows of a line load the same chunk
+// entries, so the per-row broadcasts serve the whole line.
+template <int DPL, bool EXACT, int DX, bool PRIO = false, int LPL = 16>
 __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                           uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g,
                                           int y0)
 {
+    static_assert(LPL == 16 || LPL == 32, "horizontal scans: 16- or 32-lane lines");
     constexpr int M = DPL / 2;
     constexpr int U = DPL > 16 ? DPL : 16;       // unroll: window rotation period and chunk size
     const int lane = threadIdx.x & 63;
-    const int r = lane >> 4, p = lane & 15;
+    const int r = lane / LPL, p = lane % LPL;
     const int y = y0 + r;
     const bool rowok = y < g.H;
     const int yc = min(y, g.H - 1);
@@ -395,30 +417,30 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
     uint8_t* tr = trash + lane * DPL;
     const bool lane_ok = rowok && (EXACT || p * DPL < g.D);
     const bool hi_ok = EXACT || p * DPL + 16 < g.D;            // DPL == 32 only
-    HChunk16 cur = hload16<DPL, DX>(cLr, cRr, g, 0, p);
+    HChunk16 cur = hload16<DPL, DX, LPL>(cLr, cRr, g, 0, lane & 15);
     HChunk16 nxt = cur;
     for (int b = 0; b * U < n; b++) {
         if constexpr (PRIO) lr_prio(((n - b * U) * SGM_LRPRIO_HW) >> 6, g.H);   // a scan step ~0.58 row steps
         static_for<0, U>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
-            if constexpr (t % 16 == 0) nxt = hload16<DPL, DX>(cLr, cRr, g, (b * U + t) / 16 + 1, p);
+            if constexpr (t % 16 == 0) nxt = hload16<DPL, DX, LPL>(cLr, cRr, g, (b * U + t) / 16 + 1, lane & 15);
             const int i = b * U + t;
             const uint64_t cl = row_bcast_u64<t % 16>(cur.cl);
             const uint64_t inj = row_bcast_u64<t % 16>(cur.inj);
             // logical window index k lives in physical register (k - t) (DX>0) / (k + t) (DX<0)
             uint32_t Labs[M];
-            p16_step<DPL, EXACT>(Lr, cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; },
-                                 P1P1, P2P2, imask, Labs);
+            p16_step<DPL, EXACT, LPL>(Lr, cl, [&](int k) { return cr[DX > 0 ? ((k - t) % DPL + DPL) % DPL : (k + t) % DPL]; },
+                                      P1P1, P2P2, imask, Labs);
             const int x1 = DX > 0 ? i : n - 1 - i;
             const bool ok = lane_ok && i < n;
             uint8_t* dst = ok ? rowbase + (size_t)x1 * g.D : tr;
             store_pairs<DPL>(dst, (ok && hi_ok) ? dst + 16 : tr + 16, Labs);
             if constexpr (DX > 0) {
                 constexpr int ph = ((DPL - 1 - t) % DPL + DPL) % DPL;
-                cr[ph] = row_shr1_u64(cr[ph], inj);
+                cr[ph] = LPL == 32 ? line32_shr1_u64(cr[ph], inj) : row_shr1_u64(cr[ph], inj);
             } else {
                 constexpr int ph = t % DPL;
-                cr[ph] = row_shl1_u64(cr[ph], inj);
+                cr[ph] = LPL == 32 ? line32_shl1_u64(cr[ph], inj) : row_shl1_u64(cr[ph], inj);
             }
             if constexpr (t % 16 == 15) cur = nxt;
         });
@@ -430,30 +452,30 @@ __device__ __forceinline__ void p16_horiz(const uint64_t* __restrict__ cL, const
 // line is one 16-lane row (slot j = 4*wave + row). LPL = 8: a 16-lane row holds two lines,
 // interleaved by lane parity (lane = 2*p + line), so a line's d-neighbour lanes are 2 apart
 // and its min over D stays inside the parity (p16_step, line_min_u32); slot j =
-// 8*wave + 2*row + parity. Each step the WG stages the row's right-code segment
+// 8*wave + 2*row + parity. LPL = 32: a line is a row pair (slot j = 2*wave + half). Each step the WG stages the row's right-code segment
 // (LPL*DPL + NL - 1 codes) and the NL left codes in LDS, double-buffered, one barrier per
 // step. The segment is padded so that the lanes' strided window reads spread over the
-// banks (LPL 16: one code per 16, a lane stride of 17 codes; LPL 8: four codes per 32, a
-// lane stride of 36 codes = 8 banks, conflict-free for the four lines of a 32-lane half).
+// banks (LPL 16 and 32: one code per 16, a lane stride of 17 codes; LPL 8: four codes per
+// 32, a lane stride of 36 codes = 8 banks, conflict-free for the four lines of a 32-lane half).
 template <int DPL, int LPL>
 struct RowSeg {
     static constexpr int NL = kWG / LPL;                     // lines per workgroup
     static constexpr int NSEG = LPL * DPL + NL - 1;
-    static constexpr int NPAD = LPL == 16 ? NSEG + NSEG / 16 + 1 : NSEG + 4 * (NSEG / 32) + 4;
+    static constexpr int NPAD = LPL >= 16 ? NSEG + NSEG / 16 + 1 : NSEG + 4 * (NSEG / 32) + 4;
     static constexpr int NTOT = NSEG + NL;                   // codes staged per step
     static constexpr int NLOAD = (NTOT + kWG - 1) / kWG;     // per thread
     static constexpr int BUF = NPAD + NL + kWG;              // + cL + dummy slots
-    static __device__ __forceinline__ int phys(int e) { return LPL == 16 ? e + (e >> 4) : e + 4 * (e >> 5); }
+    static __device__ __forceinline__ int phys(int e) { return LPL >= 16 ? e + (e >> 4) : e + 4 * (e >> 5); }
 };
-// row-sweep geometry for a 16-lane DPL: D <= 256 sweeps with 8 lanes per line (twice the
-// disparities per lane: the per-step overhead and the row's code reads are shared by 32
-// lines), D = 512 keeps 16 lanes (a 32-disparity lane already)
+// row-sweep geometry for a 16-lane DPL: LineCfg's lines, or with SGM_ROWS_LPL8 D <= 256
+// sweeps with 8 lanes per line (twice the disparities per lane: the per-step overhead and the
+// row's code reads are shared by 32 lines; measured slower)
 template <int DPL16>
 struct RowsCfg {
 #if SGM_ROWS_LPL8
-    static constexpr int LPL = DPL16 <= 16 ? 8 : 16;
+    static constexpr int LPL = DPL16 <= 16 ? 8 : LineCfg<DPL16>::LPL;
 #else
-    static constexpr int LPL = 16;
+    static constexpr int LPL = LineCfg<DPL16>::LPL;
 #endif
     static constexpr int DPL = DPL16 * 16 / LPL;
     static constexpr int NL = kWG / LPL;
@@ -562,8 +584,8 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int r = lane >> 4;
-    const int p = LPL == 16 ? lane & 15 : (lane & 15) >> 1;            // lane within the line
-    const int j = LPL == 16 ? 4 * w + r : 8 * w + 2 * r + (lane & 1);  // slot (line) of the lane
+    const int p = LPL == 32 ? lane & 31 : LPL == 16 ? lane & 15 : (lane & 15) >> 1;    // lane within the line
+    const int j = LPL == 32 ? 2 * w + (lane >> 5) : LPL == 16 ? 4 * w + r : 8 * w + 2 * r + (lane & 1);   // slot (line)
     const int rx = dir_rx(dir), ry = dir_ry(dir);
     int s0, s1;
     if (rx == 0) { s0 = 0; s1 = g.H; }
@@ -701,8 +723,8 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     }
 }
 
-// One work-list entry: the lines of one block of one direction of one frame (16 rows for
-// the horizontal scans, RowsCfg<DPL>::NL columns for the row sweeps; lds: rows_lds_codes).
+// One work-list entry: the lines of one block of one direction of one frame (LineCfg<DPL>::HROWS
+// rows for the horizontal scans, RowsCfg<DPL>::NL columns for the row sweeps; lds: rows_lds_codes).
 template <int DPL>
 __host__ __device__ constexpr int rows_lds_codes() { return 2 * RowSeg<RowsCfg<DPL>::DPL, RowsCfg<DPL>::LPL>::BUF; }
 
@@ -711,6 +733,7 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
                                               const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
     using RC = RowsCfg<DPL>;
+    using HC = LineCfg<DPL>;
     const int dir = (int)(it >> 24);
     const int f = (int)((it >> 22) & 3u);
     const int lb = (int)(it & 0x3FFFFFu);
@@ -719,8 +742,9 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     const uint64_t* cR = pick4(pf.cR, f);
     uint8_t* V = pick4(pf.vols, f) + (size_t)dir * vol_bytes;
     uint8_t* trash = V + trash_off;
-    if (dir == 6) p16_horiz<DPL, EXACT, 1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
-    else if (dir == 7) p16_horiz<DPL, EXACT, -1, PRIO>(cL, cR, V, trash, g, lb * kRowsPerWG + 4 * (threadIdx.x >> 6));
+    const int y0 = lb * HC::HROWS + (64 / HC::LPL) * (threadIdx.x >> 6);
+    if (dir == 6) p16_horiz<HC::DPL, EXACT, 1, PRIO, HC::LPL>(cL, cR, V, trash, g, y0);
+    else if (dir == 7) p16_horiz<HC::DPL, EXACT, -1, PRIO, HC::LPL>(cL, cR, V, trash, g, y0);
     else p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
 }
 
@@ -736,7 +760,7 @@ __device__ __forceinline__ void trace_record(uint64_t* trace, uint64_t tag, uint
 }
 
 template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 ? SGM_WPE32 : SGM_WPE)))
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(DPL >= 32 && !SGM_P32 ? SGM_WPE32 : SGM_WPE)))
 void k_census_paths16(PathFrames pf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
                       const uint32_t* __restrict__ items, uint64_t* __restrict__ trace)
 {
@@ -1095,6 +1119,8 @@ static int rows_lines(int D)
     default: return RowsCfg<32>::NL;
     }
 }
+// image rows per horizontal-scan workgroup (LineCfg<DPL>::HROWS of the launch's DPL)
+static int hscan_rows(int D) { return dpl16_for(D) == 32 ? LineCfg<32>::HROWS : LineCfg<16>::HROWS; }
 
 PathLaunch16 make_path_launch16(const Geom& g)
 {
@@ -1127,7 +1153,7 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
     for (int dir = 0; dir < 8; dir++) {
         if (!((dir_mask >> dir) & 1u)) continue;
         if (dir >= 6) {
-            const int nb = (g.H + kRowsPerWG - 1) / kRowsPerWG;
+            const int nb = (g.H + hscan_rows(g.D) - 1) / hscan_rows(g.D);
             for (int b = 0; b < nb; b++)
                 for (int f = 0; f < group; f++) v.push_back({g.width1, path_item(dir, b, f)});
             continue;

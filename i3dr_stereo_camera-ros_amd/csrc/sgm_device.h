@@ -408,15 +408,37 @@ __device__ __forceinline__ uint32_t row_shl_n(uint32_t v, uint32_t old) {
 }
 // unsigned min over the lanes of one path line, result in every lane of the line:
 // LPL = 16: the whole 16-lane row; LPL = 8: the lanes of one parity in the row (two
-// interleaved lines per row, lane = 2 * p + line)
+// interleaved lines per row, lane = 2 * p + line); LPL = 32: a row pair (rows 0-1, 2-3),
+// the two row minima joined by v_permlane16_swap
 template <int LPL>
 __device__ __forceinline__ uint32_t line_min_u32(uint32_t v) {
-    if constexpr (LPL == 16)
+    if constexpr (LPL >= 16)
         v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
     v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, true));       // quad_perm [2,3,0,1]
     v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, true));      // row_ror:4
     v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, true));      // row_ror:8
+    if constexpr (LPL == 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);         // rows (0,1), (2,3) exchanged
+        v = min((uint32_t)sw[0], (uint32_t)sw[1]);
+    }
     return v;
+}
+// neighbour lanes inside 32-lane lines (lane i <- i - 1 / i + 1 across the row boundary of
+// the line; the line's first / last lane reads `old`): wave_shr/shl:1 + one select for the
+// lane that would read the other line of the wave
+__device__ __forceinline__ uint32_t line32_shr1(uint32_t v, uint32_t old) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+    return (threadIdx.x & 31) == 0 ? old : t;
+}
+__device__ __forceinline__ uint32_t line32_shl1(uint32_t v, uint32_t old) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+    return (threadIdx.x & 31) == 31 ? old : t;
+}
+__device__ __forceinline__ uint64_t line32_shr1_u64(uint64_t v, uint64_t old) {
+    return ((uint64_t)line32_shr1((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) | line32_shr1((uint32_t)v, (uint32_t)old);
+}
+__device__ __forceinline__ uint64_t line32_shl1_u64(uint64_t v, uint64_t old) {
+    return ((uint64_t)line32_shl1((uint32_t)(v >> 32), (uint32_t)(old >> 32)) << 32) | line32_shl1((uint32_t)v, (uint32_t)old);
 }
 // unsigned min over the 16 lanes of each row, result in every lane of the row
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {

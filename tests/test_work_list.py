@@ -1,14 +1,15 @@
 """Host logic of the census path launch (no GPU): the work list a fused launch dispatches
-(census_sgm.hip census_path_items, exported as sgm_debug_path_items). Every 16-line block of
-every requested direction of every frame appears exactly once, the up+WTA blocks (code 8:
-the dir-1 column blocks, fused with the WTA) of the WTA group likewise, and the longest work
-(the up+WTA chains) is dealt first."""
+(census_sgm.hip census_path_items, exported as sgm_debug_path_items). Every block of every
+requested direction of every frame appears exactly once, the up+WTA blocks (code 8: the
+dir-1 column blocks, fused with the WTA) of the WTA group likewise, and the longest work
+(the up+WTA chains) is dealt first. Blocks hold 16 lines (16 rows for the horizontal scans),
+8 for D > 256, whose path lines are 32 lanes wide (census_sgm.hip LineCfg); up+WTA blocks
+always 16."""
 import ctypes
 
 import numpy as np
 import pytest
 
-NL = 16          # lines per row-sweep block / rows per horizontal block
 
 
 def items(pkg, W, H, D, minD, mask, slots, group, up):
@@ -22,9 +23,10 @@ def items(pkg, W, H, D, minD, mask, slots, group, up):
     return out[:n]
 
 
-def expected_blocks(W, H, D, minD, d):
+def expected_blocks(W, H, D, minD, d, NL=None):
     """Blocks per direction: the row sweeps cover their lines' start columns (diagonals
-    reach H - 1 columns further), the horizontal scans 16 rows each."""
+    reach H - 1 columns further), the horizontal scans NL rows each."""
+    NL = NL or (8 if D > 256 else 16)      # lines per row-sweep block / rows per horizontal block
     minX1, maxX1 = max(minD + D, 0), W + min(minD, 0)
     if d >= 6:
         return (H + NL - 1) // NL
@@ -44,7 +46,7 @@ def test_work_list_covers_every_block_once(pkg, W, H, D, minD, group, up, slots)
     seen = set(zip(code.tolist(), f.tolist(), lb.tolist()))
     assert len(seen) == len(it)                                    # no duplicates
     want = {(d, fr, b) for d in range(8) for fr in range(group) for b in range(expected_blocks(W, H, D, minD, d))}
-    want |= {(8, fr, b) for fr in range(up) for b in range(expected_blocks(W, H, D, minD, 1))}
+    want |= {(8, fr, b) for fr in range(up) for b in range(expected_blocks(W, H, D, minD, 1, NL=16))}
     assert seen == want
     n_up = int((code == 8).sum())
     if n_up:                                                       # the longest chains lead
