@@ -328,16 +328,11 @@ __device__ __forceinline__ void make_imask(int p, int D, uint32_t (&imask)[DPL /
 // directions 0, 2, 3 (slots 0, 1, 2), bnd[1] the first row of the band below for the upward
 // directions 1, 4, 5; each slot is width1 * D u8 costs in volume order, bnd_slot bytes
 // apart. Null: the band edge is the image edge (lines start there).
-// Split single frame (sgm_api.cpp run_pipeline): the row sweeps of a launch run only the
-// steps [s_lo, s_hi) of their lines; a line that began in an earlier launch continues from
-// the u8 costs that launch stored for its predecessor pixel in the same volume (p16_seed).
 struct PathLaunch16 {
     int xb_lo[6];        // row sweeps: first base column of the direction
     const uint8_t* bnd[2];
     size_t bnd_slot;
-    int s_lo, s_hi;      // row sweeps: step window of this launch (0, kAllSteps: whole lines)
 };
-constexpr int kAllSteps = 1 << 30;
 __host__ __device__ constexpr int bnd_slot_of(int dir) { return dir <= 1 ? 0 : (dir == 2 || dir == 4 ? 1 : 2); }
 // Work list entry (one per workgroup): dir << 24 | frame-in-group << 22 | local block.
 __host__ __device__ constexpr uint32_t path_item(int dir, int lb, int f = 0)
@@ -596,9 +591,6 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     if (rx == 0) { s0 = 0; s1 = g.H; }
     else if (rx > 0) { s0 = max(0, g.minX1 - xb - (NL - 1)); s1 = min(g.H, g.maxX1 - xb); }
     else { s0 = max(0, xb - g.maxX1 + 1); s1 = min(g.H, xb + NL - g.minX1); }
-    const bool resumed = !FUSE && s0 < pl.s_lo;   // the lines began in an earlier launch
-    s0 = max(s0, pl.s_lo);
-    s1 = min(s1, pl.s_hi);
     if (s0 >= s1) return;                          // uniform over the workgroup
     uint32_t imask[M], start[M];
     make_imask<DPL, EXACT>(p, g.D, imask, start);
@@ -607,17 +599,13 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 #pragma unroll
     for (int i = 0; i < M; i++) Lr[i] = start[i];
     bool pv = false;
-    // predecessor row of step s0: the previous launch's last row of this volume (split single
-    // frame), or the neighbouring band's boundary row (exact tile mode)
-    const uint8_t* seed = nullptr;
-    if (resumed) seed = V + (size_t)(ry > 0 ? s0 - 1 : g.H - s0) * g.width1 * g.D;
-    else if (pl.bnd[ry > 0 ? 0 : 1] && s0 == 0) seed = pl.bnd[ry > 0 ? 0 : 1] + bnd_slot_of(dir) * pl.bnd_slot;
-    if (seed) {
-        const int x = xb + j + rx * s0, xp = x - rx;   // the line's pixel at step s0 and its predecessor
+    const uint8_t* bnd = pl.bnd[ry > 0 ? 0 : 1];
+    if (bnd && s0 == 0) {                          // exact tile mode: continue the band above / below
+        const int x = xb + j, xp = x - rx;         // the line's pixel at step 0 and its predecessor
         const bool cont = x >= g.minX1 && x < g.maxX1 && xp >= g.minX1 && xp < g.maxX1;
         const int xs = min(max(xp, g.minX1), g.maxX1 - 1) - g.minX1;
         uint32_t Ls[M];
-        p16_seed<DPL, EXACT, LPL>(seed + (size_t)xs * g.D + p * DPL, imask, Ls);
+        p16_seed<DPL, EXACT, LPL>(bnd + bnd_slot_of(dir) * pl.bnd_slot + (size_t)xs * g.D + p * DPL, imask, Ls);
 #pragma unroll
         for (int i = 0; i < M; i++) Lr[i] = cont ? Ls[i] : Lr[i];
         pv = cont;
@@ -961,15 +949,13 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
     row_finish(g, tid, kWG, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
-// block b: row i = b % N of frame b / N (N rows per frame: all H, or the wf.rows_* segments)
+// block b: row b % H of frame b / H
 template <int DPL, bool EXACT>
 __device__ __forceinline__ void wta_block16(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride,
                                             int b, uint32_t* lds)
 {
-    const int N = wta_rows_per_frame(wf.rows_n, g.H);
-    const int f = b / N, i = b - f * N;
-    const int y = wf.rows_n <= 0 ? i : (i < wf.rows_n0 ? wf.rows_lo0 + i : wf.rows_lo1 + (i - wf.rows_n0));
-    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, y, lds);
+    const int f = b / g.H;
+    wta_row16<DPL, EXACT>(pick4(wf.vols, f), vol_bytes, g, pick4(wf.out, f), out_stride, b - f * g.H, lds);
 }
 
 template <int DPL, bool EXACT>
@@ -1051,7 +1037,7 @@ void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_b
     extern __shared__ uint64_t lds_dyn64[];
     const uint64_t t0 = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const int b = blockIdx.x;
-    const int n_wta = wta_rows ? wta_rows_per_frame(wf.rows_n, g.H) * wf.n : 0;
+    const int n_wta = wta_rows ? g.H * wf.n : 0;
     // paths and WTA blocks merged: among the first b+1 blocks, wcount(b) are WTA rows
     // (one in period16/16 blocks, period16 = 0: all WTA rows after the paths)
     auto wcount = [&](int bb) {
@@ -1140,8 +1126,6 @@ PathLaunch16 make_path_launch16(const Geom& g)
 {
     PathLaunch16 pl{};
     for (int dir = 0; dir < 6; dir++) pl.xb_lo[dir] = g.minX1 - (dir_rx(dir) > 0 ? g.H - 1 : 0);
-    pl.s_lo = 0;
-    pl.s_hi = kAllSteps;
     return pl;
 }
 
@@ -1152,10 +1136,8 @@ PathLaunch16 make_path_launch16(const Geom& g)
 // short work; with group > 1 there are more blocks than resident slots and the dispatcher
 // hands the short ones to whichever CUs drain first).
 // up_group > 0 adds the up+WTA blocks (dir code 8, the dir-1 column blocks) of that many
-// frames of the launch's WTA group, first: they are the longest. [s_lo, s_hi): the row
-// sweeps' step window of the launch (PathLaunch16); blocks with no step in it are left out.
-int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, uint32_t* out, int cap, int up_group,
-                      int s_lo, int s_hi)
+// frames of the launch's WTA group, first: they are the longest.
+int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, uint32_t* out, int cap, int up_group)
 {
     struct Item { int len; uint32_t code; };
     std::vector<Item> v;
@@ -1186,10 +1168,7 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
             if (rx == 0) { s0 = 0; s1 = g.H; }
             else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (NL - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
             else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + NL - g.minX1); }
-            s0 = std::max(s0, s_lo);
-            s1 = std::min(s1, s_hi);
-            if (s0 >= s1) continue;
-            for (int f = 0; f < group; f++) v.push_back({s1 - s0, path_item(dir, b, f)});
+            for (int f = 0; f < group; f++) v.push_back({std::max(s1 - s0, 0), path_item(dir, b, f)});
         }
     }
     const int n = (int)v.size();
@@ -1260,12 +1239,10 @@ static void launch_paths_dpl(const PathFrames& pf, size_t vol_bytes, size_t tras
 // bnd_down / bnd_up (exact tile mode, may be null): see PathLaunch16.
 hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geom& g, const uint32_t* items,
                                int n_items, hipStream_t st, const uint8_t* bnd_down, const uint8_t* bnd_up,
-                               size_t bnd_slot, int s_lo, int s_hi)
+                               size_t bnd_slot)
 {
     if (n_items <= 0) return hipSuccess;
     PathLaunch16 pl = make_path_launch16(g);
-    pl.s_lo = s_lo;
-    pl.s_hi = s_hi;
     pl.bnd[0] = bnd_down;
     pl.bnd[1] = bnd_up;
     pl.bnd_slot = bnd_slot;
@@ -1283,7 +1260,7 @@ hipError_t launch_census_paths(const PathFrames& pf, size_t vol_bytes, const Geo
 template <int DPL>
 static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g, size_t out_stride, hipStream_t st)
 {
-    dim3 grid(wta_rows_per_frame(wf.rows_n, g.H) * wf.n), block(kWG);
+    dim3 grid(g.H * wf.n), block(kWG);
     const size_t lds = wta_lds_bytes<DPL>(g.W);
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
@@ -1310,7 +1287,7 @@ static void launch_fused_dpl(const PathFrames& pf, const WtaFrames& wf, const Ce
                              int n_items, size_t out_stride, bool up_wta, hipStream_t st)
 {
     const int n_census = ((g.W + 63) / 64) * ((g.H + kCensusRows - 1) / kCensusRows) * 2 * cf.n;
-    dim3 grid(n_items + (up_wta ? 0 : wta_rows_per_frame(wf.rows_n, g.H) * wf.n) + n_census), block(kWG);
+    dim3 grid(n_items + (up_wta ? 0 : g.H * wf.n) + n_census), block(kWG);
     const size_t lds = std::max({up_wta ? upwta_lds_bytes<DPL>() : wta_lds_bytes<DPL>(g.W),
                                  sizeof(uint64_t) * rows_lds_codes<DPL>(), (size_t)(kCensusRows + 6) * 72});
     uint64_t* tr = trace_buffer((int)grid.x);
@@ -1343,11 +1320,9 @@ hipError_t launch_census_tiles(const CensusFrames& cf, int W, int H, hipStream_t
 // launch_census_rowfin finishes the rows) instead of WTA rows.
 hipError_t launch_census_fused(const PathFrames& pf, const WtaFrames& wf, const CensusFrames& cf, size_t vol_bytes,
                                const Geom& g, const uint32_t* items, int n_items, size_t out_stride, bool up_wta,
-                               hipStream_t st, int s_lo, int s_hi)
+                               hipStream_t st)
 {
-    PathLaunch16 pl = make_path_launch16(g);
-    pl.s_lo = s_lo;
-    pl.s_hi = s_hi;
+    const PathLaunch16 pl = make_path_launch16(g);
     const size_t trash_off = (size_t)g.H * g.width1 * g.D;
     switch (dpl16_for(g.D)) {
     case 2: launch_fused_dpl<2>(pf, wf, cf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, up_wta, st); break;

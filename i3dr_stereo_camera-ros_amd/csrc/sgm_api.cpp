@@ -24,12 +24,9 @@
 
 namespace sgm {
 hipError_t launch_census(const uint8_t*, const uint8_t*, size_t, int, int, uint64_t*, uint64_t*, hipStream_t);
-constexpr int kAllSteps = 1 << 30;   // census_sgm.hip: a step window covering whole lines
-int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int, int up_group = 0, int s_lo = 0,
-                      int s_hi = kAllSteps);
+int census_path_items(const Geom&, unsigned, int, int, uint32_t*, int, int up_group = 0);
 hipError_t launch_census_paths(const PathFrames&, size_t, const Geom&, const uint32_t*, int, hipStream_t,
-                               const uint8_t* = nullptr, const uint8_t* = nullptr, size_t = 0, int s_lo = 0,
-                               int s_hi = kAllSteps);
+                               const uint8_t* = nullptr, const uint8_t* = nullptr, size_t = 0);
 hipError_t launch_census_wta(const WtaFrames&, size_t, const Geom&, size_t, hipStream_t);
 hipError_t launch_rectify_map(const double*, const double*, const double*, int, int, float*, float*, size_t,
                               hipStream_t);
@@ -39,7 +36,7 @@ void cubic_table(int16_t*);
 bool rectify_inverse(const double*, const double*, double*);
 hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
-                               const uint32_t*, int, size_t, bool, hipStream_t, int s_lo = 0, int s_hi = kAllSteps);
+                               const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
@@ -164,7 +161,7 @@ struct sgm_handle {
     size_t aux_n = 0;
     uint32_t* items_pin = nullptr; // pinned host copy of the uploaded path work list
     int items_cap = 0;
-    std::string items_key[3];      // geometry + workspace each device copy (single / group / split) belongs to
+    std::string items_key[2];      // geometry + workspace each device copy (single / group) belongs to
     int16_t* cubic_tab = nullptr;  // device INTER_CUBIC weight table (sgm_remap_cubic), built once
     bool rect_on = false;          // sgm_set_rectification: batch inputs are raw, rectified in the census
     sgm::RectifyIn rect{};
@@ -259,7 +256,8 @@ int stage_index(sgm_handle* h, const char* name, double bytes)
 int ensure_ws(sgm_handle* h, size_t bytes)
 {
     if (h->ws.size >= bytes) return SGM_OK;
-    for (auto& k : h->items_key) k.clear();   // contents (the path work lists) do not survive
+    h->items_key[0].clear();       // contents (the path work lists) do not survive
+    h->items_key[1].clear();
     if (h->ws.base) {
         (void)hipStreamSynchronize(h->stream);
         if (h->done_stream) (void)hipEventSynchronize(h->done);
@@ -311,8 +309,7 @@ struct Layout {
     size_t vol_bytes = 0;
     int group = 1;                                         // frames per pipelined launch
     bool up_wta = false;                                   // pipelined batch: up+WTA scheme
-    size_t items[3] = {}; int n_items[3] = {};             // path work lists: one frame / a group / a
-                                                           // split single frame's second launch
+    size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0, outf = 0;            // host-API staging (int16 / float out)
@@ -356,8 +353,6 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         if (g.width1 > 0) {
             l.n_items[0] = sgm::census_path_items(g, 0xFFu, 1, 1, nullptr, 0);
             l.items[0] = take((size_t)l.n_items[0] * 4);
-            l.n_items[2] = l.n_items[0];                   // any step window's list is a subset
-            l.items[2] = take((size_t)l.n_items[2] * 4);
             if (group > 0) {
                 l.n_items[1] = sgm::census_path_items(g, 0xFFu, 1, l.group, nullptr, 0, l.up_wta ? l.group : 0);
                 l.items[1] = take((size_t)l.n_items[1] * 4);
@@ -406,19 +401,18 @@ struct StageRec {
     }
 };
 
-// Device work list of the census path launch for (g, dir_mask, step window), uploaded on
-// `st` when the geometry or the workspace changed. slot: 0 single frame, 1 group, 2 the second
-// launch of a split single frame (-1: by group). Returns the entry count (< 0: error).
+// Device work list of the census path launch for (g, only_dir), uploaded on `st` when the
+// geometry or the workspace changed. Returns the entry count (< 0: error).
 int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask, int group, hipStream_t st,
-               const uint32_t** dev, int up_group = 0, int slot = -1, int s_lo = 0, int s_hi = sgm::kAllSteps)
+               const uint32_t** dev, int up_group = 0)
 {
-    const int w = slot >= 0 ? slot : (group > 1 || up_group > 0 ? 1 : 0);
+    const int w = group > 1 || up_group > 0 ? 1 : 0;
     uint32_t* d = (uint32_t*)((char*)h->ws.base + l.items[w]);
     *dev = d;
-    char key[192];
-    snprintf(key, sizeof key, "%d %d %d %d %x %d %d %d %p %d %d", g.W, g.H, g.D, g.minD, dir_mask, group, up_group,
-             h->n_cu, (void*)d, s_lo, s_hi);
-    const int n = sgm::census_path_items(g, dir_mask, h->n_cu, group, nullptr, 0, up_group, s_lo, s_hi);
+    char key[160];
+    snprintf(key, sizeof key, "%d %d %d %d %x %d %d %d %p", g.W, g.H, g.D, g.minD, dir_mask, group, up_group, h->n_cu,
+             (void*)d);
+    const int n = sgm::census_path_items(g, dir_mask, h->n_cu, group, nullptr, 0, up_group);
     if (h->items_key[w] == key) return n;
     if (n > l.n_items[w]) return fail(h, SGM_ERR_ARG, "path work list larger than its workspace slot");
     if (n > h->items_cap) {
@@ -428,7 +422,7 @@ int path_items(sgm_handle* h, const Layout& l, const Geom& g, unsigned dir_mask,
         HIP_TRY(hipHostMalloc((void**)&h->items_pin, (size_t)n * 4, hipHostMallocDefault), "hipHostMalloc");
         h->items_cap = n;
     }
-    sgm::census_path_items(g, dir_mask, h->n_cu, group, h->items_pin, h->items_cap, up_group, s_lo, s_hi);
+    sgm::census_path_items(g, dir_mask, h->n_cu, group, h->items_pin, h->items_cap, up_group);
     HIP_TRY(hipMemcpyAsync(d, h->items_pin, (size_t)n * 4, hipMemcpyHostToDevice, st), "H2D items");
     HIP_TRY(hipStreamSynchronize(st), "sync");    // geometry changes are rare: never leave the pinned copy in flight
     h->items_key[w] = key;
@@ -460,29 +454,6 @@ int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_
     return SGM_OK;
 }
 
-// Split single census frame (run_pipeline): steps of the row sweeps in the first launch, or 0
-// for the one-launch schedule (paths8 then wta_lr). The WTA rows of the middle band, complete
-// after the first launch, then run beside the sweeps' last steps: the path sweeps are
-// VALU-bound and the WTA HBM-bound, so they overlap. The first launch must also finish the
-// horizontal scans (width1 steps at ~0.58 of a row step), so the split pays only on frames
-// that are tall for their width (C5: 4096x3000). SGM_SPLIT: 0 off, a fraction in (0.5, 1)
-// forces S1 = fraction * H (parity tests), unset: automatic.
-int split_steps(const Geom& g)
-{
-    double f;
-    const char* e = std::getenv("SGM_SPLIT");
-    if (e) {
-        f = std::atof(e);
-        if (!(f > 0.5 && f < 1.0)) return 0;
-    } else {
-        if (g.H < 1024) return 0;
-        f = std::max(0.62, 0.58 * g.width1 / g.H + 0.03);
-        if (f > 0.8) return 0;
-    }
-    const int S1 = (int)(f * g.H);
-    return S1 > g.H / 2 && S1 < g.H ? S1 : 0;
-}
-
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
                  int16_t* dOut, size_t out_stride)
@@ -508,43 +479,17 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
         rec.begin("census", 2 * WH + 16 * WH);
         HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
-        const int S1 = split_steps(g);
         const uint32_t* items;
-        const int n_items = path_items(h, l, g, 0xFFu, 1, st, &items, 0, 0, 0, S1 > 0 ? S1 : sgm::kAllSteps);
+        const int n_items = path_items(h, l, g, 0xFFu, 1, st, &items);
         if (n_items < 0) return n_items;
         sgm::PathFrames pf{};
         pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
         sgm::WtaFrames wf{};
         wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
-        if (S1 == 0) {
-            rec.begin("paths8", 8 * cells);
-            HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
-            rec.begin("wta_lr", 8 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
-        } else {
-            // split single frame: (a) every direction, the row sweeps for their first S1 steps;
-            // (b) the row sweeps' last H - S1 steps beside the WTA rows of the middle band
-            // [H - S1, S1), complete after (a); (c) the WTA rows of the two outer bands
-            const uint32_t* items_b;
-            const int n_b = path_items(h, l, g, 0x3Fu, 1, st, &items_b, 0, 2, S1, sgm::kAllSteps);
-            if (n_b < 0) return n_b;
-            const double fa = (double)S1 / g.H, mid = 2.0 * S1 - g.H;
-            sgm::WtaFrames wm = wf, wo = wf;
-            wm.rows_n = wm.rows_n0 = (int)mid;
-            wm.rows_lo0 = g.H - S1;
-            wo.rows_n = 2 * (g.H - S1);
-            wo.rows_n0 = g.H - S1;
-            wo.rows_lo0 = 0;
-            wo.rows_lo1 = S1;
-            rec.begin("paths8_a", (6 * fa + 2) * cells);
-            HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st, nullptr, nullptr, 0, 0, S1),
-                    "paths a");
-            rec.begin("paths8_b+wta_mid", 6 * (1 - fa) * cells + 8 * cells * mid / g.H + 2 * g.W * mid);
-            HIP_TRY(sgm::launch_census_fused(pf, wm, sgm::CensusFrames{}, l.vol_bytes, g, items_b, n_b, dst_stride, false,
-                                             st, S1, sgm::kAllSteps), "paths b + wta");
-            rec.begin("wta_outer", 8 * cells * wo.rows_n / g.H + 2.0 * g.W * wo.rows_n);
-            HIP_TRY(sgm::launch_census_wta(wo, l.vol_bytes, g, dst_stride, st), "wta outer");
-        }
+        rec.begin("paths8", 8 * cells);
+        HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
+        rec.begin("wta_lr", 8 * cells + 2 * WH);
+        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -750,8 +695,7 @@ int prepare(sgm_handle* h, int W, int H, bool host_io, Geom& g, Layout& l, int g
     if ((rc = ensure_stream(h))) return rc;
     l = make_layout(h->params, g, host_io, group);
     // the uploaded path work list lives in the workspace: any other use of it invalidates it
-    if (h->params.mode != SGM_MODE_CENSUS8)
-        for (auto& k : h->items_key) k.clear();
+    if (h->params.mode != SGM_MODE_CENSUS8) { h->items_key[0].clear(); h->items_key[1].clear(); }
     return ensure_ws(h, l.total);
 }
 
@@ -824,7 +768,8 @@ int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H,
             HIP_TRY(hipStreamSynchronize(q->stream), "hipStreamSynchronize");
             HIP_TRY(hipFree(q->ws.base), "hipFree lane workspace");
             q->ws = Workspace{};
-            for (auto& k : q->items_key) k.clear();
+            q->items_key[0].clear();
+            q->items_key[1].clear();
         }
     }
     return SGM_OK;
@@ -1652,7 +1597,6 @@ int band_prepare(sgm_handle* b, const Geom& g, const BandLayout& l)
     }
     b->items_key[0] = key;
     b->items_key[1].clear();
-    b->items_key[2].clear();
     return SGM_OK;
 }
 

@@ -274,7 +274,6 @@ __device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, con
 // A group of frames handled by one launch (frame pipelining): per frame its census codes
 // and volume set (paths) or volume set and output (WTA). Frames >= n are skipped.
 constexpr int kMaxGroup = 4;
-__host__ __device__ inline int wta_rows_per_frame(int rows_n, int H) { return rows_n > 0 ? rows_n : H; }
 struct PathFrames {
     const uint64_t* cL[kMaxGroup];
     const uint64_t* cR[kMaxGroup];
@@ -286,9 +285,6 @@ struct WtaFrames {
     const uint8_t* vols[kMaxGroup];
     int16_t* out[kMaxGroup];
     int n;
-    // WTA rows of each frame: all H (rows_n = 0), or rows_n rows: [lo0, lo0 + n0) then from lo1
-    // (a split single frame's middle band, and its two outer bands)
-    int rows_n, rows_n0, rows_lo0, rows_lo1;
     // up+WTA blocks (census_sgm.hip UpWta): the frames' codes and per-pixel result images
     const uint64_t* cL[kMaxGroup];
     const uint64_t* cR[kMaxGroup];

@@ -66,46 +66,6 @@ def test_census_pipeline(engine, oracle, synth, pkg, kw):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
-SPLIT_CASES = [(90, 210, dict(num_disparities=64)),
-               (77, 190, dict(num_disparities=32, min_disparity=-9, median=1)),
-               (64, 400, dict(num_disparities=256, uniqueness_ratio=5)),
-               (70, 520, dict(num_disparities=400, min_disparity=-5)),       # 32-lane lines, D < 512
-               (53, 700, dict(num_disparities=512, speckle_window_size=20, speckle_range=2)),
-               (41, 300, dict(num_disparities=128, subpixel=0, lr_check=0))]
-
-
-@pytest.mark.parametrize("frac", ["0.51", "0.6", "0.75", "0.97"])
-@pytest.mark.parametrize("h,w,kw", SPLIT_CASES, ids=[str(i) for i in range(len(SPLIT_CASES))])
-def test_census_split_single_frame(engine, oracle, synth, pkg, monkeypatch, frac, h, w, kw):
-    """Split single frame (sgm_api.cpp split_steps, forced by SGM_SPLIT): the row sweeps stop
-    after S1 = frac * H steps, resume in a second launch from the rows they stored (diagonal
-    lines that enter, leave or cross the window edge included), beside the WTA rows of the
-    middle band; the outer bands' WTA rows follow. Bit-exact with the oracle."""
-    monkeypatch.setenv("SGM_SPLIT", frac)
-    D, minD = kw["num_disparities"], kw.get("min_disparity", 0)
-    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h + w)
-    p = pkg.default_params(pkg.MODE_CENSUS8, **kw)
-    engine.set_params(p)
-    got = engine.match(left, right)
-    ref = oracle.match(to_oracle_params(oracle, p), left, right)
-    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
-
-
-def test_census_split_auto_tall_frame(engine, oracle, synth, pkg, monkeypatch):
-    """The automatic split (no SGM_SPLIT) takes frames tall for their width (H >= 1024 and the
-    horizontal scans short enough to finish in the first launch): 1100 x 330, D 64."""
-    monkeypatch.delenv("SGM_SPLIT", raising=False)
-    left, right, _ = synth.stereo_pair(1100, 330, 0, 64, seed=1100)
-    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=64)
-    engine.set_params(p)
-    engine.set_profiling(True)
-    got = engine.match(left, right)
-    names = [n for n, _, _ in engine.stage_times()]
-    engine.set_profiling(False)
-    assert "paths8_b+wta_mid" in names and "wta_outer" in names, names
-    assert np.array_equal(got, oracle.match(to_oracle_params(oracle, p), left, right))
-
-
 def test_census_edge_geometry(engine, oracle, pkg):
     rng = np.random.default_rng(3)
     for (h, w, D, minD) in [(4, 20, 16, 0), (3, 17, 16, 0), (9, 16, 16, 0), (30, 40, 48, 0), (2, 200, 64, -30)]:
