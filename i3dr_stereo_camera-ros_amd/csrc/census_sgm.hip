@@ -45,9 +45,6 @@
 #ifndef SGM_ROWS_LPL8
 #define SGM_ROWS_LPL8 0    // 1: row sweeps with 8 lanes per path line for D <= 256 (RowsCfg; measured slower)
 #endif
-#ifndef SGM_EDGE_OR
-#define SGM_EDGE_OR 1      // line-edge neighbours as one DPP-OR per exchange (0: DPP move + select)
-#endif
 #ifndef SGM_P32
 #define SGM_P32 1          // D > 256: 32-lane path lines of 16 disparities per lane (0: 16 lanes x 32, LineCfg)
 #endif
@@ -297,20 +294,8 @@ __device__ __forceinline__ void p16_step(uint32_t (&Lr)[DPL / 2], uint64_t cl, F
 #pragma unroll
     for (int i = 0; i < M; i++) q[i] = Lr[i] + P1P1;      // = pk_add: halves <= kInfP | kBaseP, no carry
     // previous lane: its .hi is q(d0 - 1); next lane: its .lo is q(d0 + DPL)
-#if SGM_EDGE_OR
-    // the neighbour exchange as one DPP-OR: lanes whose source is outside the row read 0, and
-    // the line's first / last lane ORs 0x7000 into the half it passes on, which makes that
-    // neighbour >= kInfP (never the minimum; the patterns stay finite f16 below 0x7C00). With
-    // 32-lane lines this also covers the lane that reads the wave's other line.
-    const int pl = (int)(threadIdx.x & (LPL == 8 ? 15 : LPL - 1));
-    const uint32_t eX = (LPL == 8 ? pl < 2 : pl == 0) ? 0x70000000u : 0u;
-    const uint32_t eY = (LPL == 8 ? pl >= 14 : pl == LPL - 1) ? 0x00007000u : 0u;
-    const uint32_t X = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[M - 1], LPL == 32 ? 0x138 : 0x110 + SH, 0xf, 0xf, true) | eX;
-    const uint32_t Y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[0], LPL == 32 ? 0x130 : 0x100 + SH, 0xf, 0xf, true) | eY;
-#else
     const uint32_t X = LPL == 32 ? line32_shr1(q[M - 1], kInfP2) : row_shr_n<SH>(q[M - 1], kInfP2);
     const uint32_t Y = LPL == 32 ? line32_shl1(q[0], kInfP2) : row_shl_n<SH>(q[0], kInfP2);
-#endif
     uint32_t Oprev = alignbit16(q[0], X);                 // (q(d-1), q(d)) for pair 0
 #pragma unroll
     for (int i = 0; i < M; i++) {
