@@ -30,6 +30,14 @@ constexpr int kMaxCost = 32767;
 #ifndef SGM_OCV_PRIO
 #define SGM_OCV_PRIO 0     // longest-remaining-first wave priority (lr_prio) in k_ocv_paths
 #endif
+#ifndef SGM_OCV_VWTA_PF
+#define SGM_OCV_VWTA_PF 3    // steps whose operands k_ocv_vwta keeps in flight (DPL <= 8)
+#endif
+#ifndef SGM_OCV_PF_WIDE32
+#define SGM_OCV_PF_WIDE32 4  // 32-lane lines with more than 4 values per lane (D > 256: the shipped
+                             // 2448x2048 D=480 config, 1 / 2 / 3 / 4 rows: MODE_SGBM 15.01 / 14.86 /
+                             // 14.80 / 14.79 ms per frame, MODE_HH 22.3 / 21.9 / 21.55 / 21.5)
+#endif
 #ifndef SGM_OCV_PF_WIDE
 #define SGM_OCV_PF_WIDE 2  // the same for more disparities per lane (1080p D=128 MODE_SGBM paths:
                            // 1 step 1.42 ms, 2 steps 0.95, 3 steps 1.57, 4 steps 1.25)
@@ -685,7 +693,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // one vector load per lane (lanes past D read the last valid group: their C never
     // reaches an entry with d < D): no exec-masked branch around the loads, so the prefetch
     // keeps counted waits
-    constexpr int PF = DPL <= 4 ? SGM_OCV_PF : SGM_OCV_PF_WIDE;
+    constexpr int PF = DPL <= 4 ? SGM_OCV_PF : LPL == 32 ? SGM_OCV_PF_WIDE32 : SGM_OCV_PF_WIDE;
     int Cb[PF][DPL];
     const bool lane_act = p * DPL < g.D;
     // 32 values per lane (64-lane lines, D > 1024) with D % 32 = 16: one lane straddles D. It
@@ -953,6 +961,115 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
     row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
+// The vertical path of OpenCV's last group fused with the WTA (`k_ocv_vwta`): MODE_SGBM's ↓
+// (dir 0, volume slot 0) or MODE_HH's ↑ (dir 1, slot 1, in pass 2) runs after the other
+// directions' volumes are complete. Each wave is one column, its 64 lanes holding the D
+// disparities (the WTA's pixel layout), so at every step the wave has L of pixel (x, y) in
+// registers: it loads the other NDIR - 1 path costs of (x, y), sums S in OpenCV's saturating
+// order (ocv_sum, with its own values in their slot) and runs the pixel's WTA (the decisions of
+// k_ocv_wta16: key-min over (S + 32768) << 11 | tie(d), per-element uniqueness, S[best +- 1]
+// by readlane). That volume is never written or read: 4 B per cell less for
+// int16 volumes. Per-pixel results (d16 | best << 16 | minS << 32, rejected: d16 = invalid,
+// best = -1) go to res; k_census_rowfin finishes the rows (disp2 + LR, the shared row_finish).
+// A column is a sequential chain of H steps and there are only width1 of them, so this pays
+// on tall frames with many columns (the shipped 2448x2048 config), not on small ones.
+template <int DPL, int NDIR, typename VT, bool SAT>
+__global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, const VT* __restrict__ vols,
+                                                 size_t vol_elems, Geom g, uint64_t* __restrict__ res)
+{
+    if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
+    constexpr int LPL = 64;                            // one column per wave: the line is the wave
+    constexpr int F = NDIR == 5 ? 0 : 1;               // the fused direction = its volume slot
+    constexpr bool kRaw = sizeof(VT) == 4;             // the volumes hold the int path costs
+    // steps whose operands are in flight (fewer for wide lanes: the register file)
+    constexpr int PF = DPL <= 8 ? SGM_OCV_VWTA_PF : DPL == 16 ? 2 : 1;
+    const int p = threadIdx.x;
+    const int x1 = blockIdx.x;
+    const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
+    const bool lane_act = p * DPL < g.D;
+    const int dl = lane_act ? p * DPL : g.D - DPL;     // lanes past D load the last group
+    auto cell = [&](int i) -> size_t {                 // cell of step i (clamped: prefetch past the end)
+        const int y = F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0);
+        return ((size_t)y * g.width1 + x1) * g.D + dl;
+    };
+    auto load = [&](int i, int (&c)[DPL], int (&v)[NDIR][DPL]) {
+        int16_t t[DPL];
+        load_i16<DPL>(C + cell(i), t);
+#pragma unroll
+        for (int k = 0; k < DPL; k++) c[k] = t[k];
+#pragma unroll
+        for (int s = 0; s < NDIR; s++)
+            if (s != F) load_vals<VT, DPL>(vols + (size_t)s * vol_elems + cell(i), v[s]);
+    };
+    int Lp[DPL], mLp = 0, Cq[PF][DPL], Vq[PF][NDIR][DPL];
+#pragma unroll
+    for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
+#pragma unroll
+    for (int q = 0; q < PF; q++) load(q, Cq[q], Vq[q]);
+    // step i: the recurrence (a chain through mLp), then the pixel's WTA, which no later step
+    // waits for: S[best +- 1] come from a readlane (best is wave-uniform), so no LDS barrier
+    // orders the steps and the WTA of one step overlaps the recurrence of the next
+    auto step = [&](int i, int (&Cc)[DPL], int (&V)[NDIR][DPL]) {
+        int L[DPL], Lraw[DPL];
+        const int lmin = ocv_step<DPL, LPL, SAT>(Cc, Lp, mLp, i > 0, p, g, L, Lraw);
+        mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            Lp[k] = L[k];
+            V[F][k] = kRaw ? Lraw[k] : L[k];           // what the volume would have held
+        }
+        int S[DPL];
+        int km = 0x7FFFFFFF;                           // keys < 2^27: signed min
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            S[k] = ocv_sum<NDIR, SAT>(V, k);
+            const int d = p * DPL + k;
+            const int key = ((S[k] + 32768) << 11) | wta_tie(d, lanetie, 11);
+            km = (lane_act && d < g.D) ? min(km, key) : km;
+        }
+        const int kmin = __builtin_amdgcn_readfirstlane(line_min_i32<LPL>(km));
+        const int best = wta_untie(kmin & 2047, lanetie, 11);
+        const int minS = (kmin >> 11) - 32768;
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < DPL; k++) {
+            const int d = p * DPL + k;
+            hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
+        }
+        // every S saturated at MAX_COST: bestDisp stays -1 in OpenCV (see k_ocv_wta16)
+        const bool rej = __ballot(hit) != 0ull || minS >= 32767;
+        auto s_at = [&](int d) {                       // S[d] of the pixel (d wave-uniform)
+            const int kk = d % DPL;
+            int v = S[0];
+#pragma unroll
+            for (int k = 1; k < DPL; k++) v = kk == k ? S[k] : v;
+            return __builtin_amdgcn_readlane(v, d / DPL);
+        };
+        const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, g.D - 1));
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const int y = F == 0 ? i : g.H - 1 - i;
+        const uint64_t v = (uint64_t)(uint16_t)(rej ? g.invalid : d16) |
+                           ((uint64_t)(uint16_t)(rej ? -1 : best) << 16) | ((uint64_t)(uint16_t)minS << 32);
+        if (p == 0 && i < g.H) __builtin_nontemporal_store(v, res + (size_t)y * g.W + g.minX1 + x1);
+    };
+    for (int i0 = 0; i0 < g.H; i0 += PF) {
+#pragma unroll
+        for (int q = 0; q < PF; q++) {
+            int Cc[DPL], V[NDIR][DPL];
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                Cc[k] = Cq[q][k];
+#pragma unroll
+                for (int s = 0; s < NDIR; s++) V[s][k] = Vq[q][s][k];
+            }
+            load(i0 + q + PF, Cq[q], Vq[q]);           // operands of step i + PF
+            step(i0 + q, Cc, V);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
@@ -985,9 +1102,10 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 }
 
 // vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 VT of trash slots
+// skipdir >= 0: that direction keeps its volume slot but launches no blocks (k_ocv_vwta runs it)
 template <int DPL, int LPL, typename VT, bool SAT>
 static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, const Geom& g, int dirmask,
-                               hipStream_t st)
+                               hipStream_t st, int skipdir)
 {
     VT* vols = (VT*)vols_;
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
@@ -999,14 +1117,15 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
         nb[i] = 0;
         if (!((dirmask >> i) & 1)) continue;
         const int lines = dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0);
-        nb[i] = (lines + 64 / LPL - 1) / (64 / LPL);
+        nb[i] = i == skipdir ? 0 : (lines + 64 / LPL - 1) / (64 / LPL);
         total += nb[i];
     }
     const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
     // 32-bit buffer offsets when a volume ends below kBufDrop (the shipped 2448x2048 D=480
     // config's int16 volumes are 3.6 GB; SGM_OCV_NO_BUF=1 forces the 64-bit path)
     const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < (size_t)kBufDrop && !getenv("SGM_OCV_NO_BUF");
-    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
+    if (total > 0)
+        hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf);
 }
 
@@ -1015,12 +1134,12 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
 // matching the frame's flag exits at once
 template <int DPL, int LPL>
 static void launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
-                               int dirmask, hipStream_t st)
+                               int dirmask, hipStream_t st, int skipdir)
 {
-    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st);
+    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st, skipdir);
     if (g.wide == 0) return;
-    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st);
-    else launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st);
+    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st, skipdir);
+    else launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st, skipdir);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
@@ -1045,25 +1164,25 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
 }
 
 hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
-                            int dirmask, hipStream_t st)
+                            int dirmask, hipStream_t st, int skipdir)
 {
     const int D = g.D;
-    const int lpl = ocv_lanes_per_line(g, dirmask);
+    const int lpl = ocv_lanes_per_line(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
     if (lpl == 64) {
-        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st);
-        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st);
+        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
     } else if (lpl == 32) {
-        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st);
-        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st);
-        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st);
-        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st);
+        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st); break;
-        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st); break;
-        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st); break;
-        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st); break;
-        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st); break;   // D <= 256 here
+        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;   // D <= 256 here
         }
     }
     return hipGetLastError();
@@ -1114,6 +1233,49 @@ hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& 
     if (g.wide == 0) return hipGetLastError();
     if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_wta_t<int16_t, true>(vols, cells, ndir, g, out, out_stride, st);
     else launch_ocv_wta_t<int32_t, false>(vols, cells, ndir, g, out, out_stride, st);
+    return hipGetLastError();
+}
+
+// Fused vertical path + WTA (k_ocv_vwta): one 64-lane line (a column) per wave, DPL = D / 64
+// rounded up to a power of two; the plain and the flagged kinds as for the paths.
+template <int DPL, int NDIR, typename VT, bool SAT>
+static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, const Geom& g, uint64_t* res,
+                              hipStream_t st)
+{
+    const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
+    hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols, vol_elems,
+                       g, res);
+}
+template <int DPL, int NDIR>
+static void launch_ocv_vwta_v(const int16_t* C, const int16_t* Csat, const void* vols, size_t cells, const Geom& g,
+                              uint64_t* res, hipStream_t st)
+{
+    if (g.wide != 1) launch_ocv_vwta_l<DPL, NDIR, int16_t, false>(C, vols, cells, g, res, st);
+    if (g.wide == 0) return;
+    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_vwta_l<DPL, NDIR, int16_t, true>(Csat, vols, cells, g, res, st);
+    else launch_ocv_vwta_l<DPL, NDIR, int32_t, false>(C, vols, cells, g, res, st);
+}
+template <int NDIR>
+static void launch_ocv_vwta_n(const int16_t* C, const int16_t* Csat, const void* vols, size_t cells, const Geom& g,
+                              uint64_t* res, hipStream_t st)
+{
+    const int D = g.D;
+    if (D <= 64) launch_ocv_vwta_v<1, NDIR>(C, Csat, vols, cells, g, res, st);
+    else if (D <= 128) launch_ocv_vwta_v<2, NDIR>(C, Csat, vols, cells, g, res, st);
+    else if (D <= 256) launch_ocv_vwta_v<4, NDIR>(C, Csat, vols, cells, g, res, st);
+    else if (D <= 512) launch_ocv_vwta_v<8, NDIR>(C, Csat, vols, cells, g, res, st);
+    else if (D <= 1024) launch_ocv_vwta_v<16, NDIR>(C, Csat, vols, cells, g, res, st);
+    else launch_ocv_vwta_v<32, NDIR>(C, Csat, vols, cells, g, res, st);
+}
+// the vertical direction of the last group (MODE_SGBM: dir 0, MODE_HH: dir 1) fused with the
+// WTA; its volume slot is never written (launch_ocv_paths with skipdir = ocv_vwta_dir(ndir))
+int ocv_vwta_dir(int ndir) { return ndir == 8 ? 1 : 0; }
+hipError_t launch_ocv_vwta(const int16_t* C, const int16_t* Csat, const void* vols, size_t cells, int ndir,
+                           const Geom& g, uint64_t* res, hipStream_t st)
+{
+    if (g.width1 <= 0) return hipSuccess;
+    if (ndir == 8) launch_ocv_vwta_n<8>(C, Csat, vols, cells, g, res, st);
+    else launch_ocv_vwta_n<5>(C, Csat, vols, cells, g, res, st);
     return hipGetLastError();
 }
 

@@ -47,7 +47,10 @@ hipError_t launch_depth_points(const float*, size_t, int, int, const float*, dou
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
-hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t);
+hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t,
+                            int skipdir = -1);
+hipError_t launch_ocv_vwta(const int16_t*, const int16_t*, const void*, size_t, int, const Geom&, uint64_t*, hipStream_t);
+int ocv_vwta_dir(int ndir);
 hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
 }  // namespace sgm
 
@@ -311,6 +314,7 @@ struct Layout {
     bool up_wta = false;                                   // pipelined batch: up+WTA scheme
     size_t items[2] = {}; int n_items[2] = {};             // path work lists: one frame / a group
     size_t planes = 0, bufA = 0, bufB = 0, ovols = 0, ovf = 0;  // ocv
+    size_t ores = 0;                                       // ocv: per-pixel results of k_ocv_vwta
     size_t tmp = 0, lab = 0, cnt = 0;                      // post
     size_t inL = 0, inR = 0, out = 0, outf = 0;            // host-API staging (int16 / float out)
     size_t total = 0;
@@ -368,6 +372,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
         l.ovols = take(es * (sgm::ocv_vol_elems(cells, es) * (p.mode == SGM_MODE_OCV_HH8 ? 8 : 5) + 64 * 32 +
                              (size_t)8 * g.D));
         l.ovf = take(sizeof(int));
+        l.ores = take(WH * 8);
     }
     l.tmp = take(WH * 2 * (size_t)std::max(group, 1));   // raw disparity before the median (per frame of a group)
     if (p.speckle_window_size > 0) { l.lab = take(WH * 4); l.cnt = take(WH * 4); }
@@ -454,6 +459,18 @@ int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_
     return SGM_OK;
 }
 
+// OpenCV modes: the vertical direction of the last group fused with the WTA (k_ocv_vwta)
+// instead of paths + k_ocv_wta16. One wave per column walks H steps and does the pixel WTAs
+// itself, so it needs frames with many cells per column chain (interleaved A/B,
+// profiles/r03_ocv_vwta_ab.jsonl, ms per frame off -> on: shipped 2448x2048 D=480 MODE_SGBM
+// 14.54 -> 13.93, MODE_HH 21.82 -> 21.63; 1080p D=128 MODE_SGBM 1.85 -> 2.11, MODE_HH 2.55 ->
+// 2.48; C1 0.23 -> 0.41). SGM_OCV_VWTA = 0 / 1 forces it off / on (parity tests run both).
+bool ocv_vwta_on(const Geom& g, int fullDP)
+{
+    if (const char* e = std::getenv("SGM_OCV_VWTA")) return std::atoi(e) != 0;
+    return (double)g.width1 * g.H * g.D >= (fullDP ? 2.0e8 : 1.0e9);
+}
+
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
                  int16_t* dOut, size_t out_stride)
@@ -506,10 +523,25 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         const double es = g.wide == 1 && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // gated: the int16 case
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
         HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, gg, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
-        rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
-        HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
-        rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
-        HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
+        if (ocv_vwta_on(g, fullDP)) {
+            // the vertical direction of the last group fused with the WTA (k_ocv_vwta), then
+            // disp2 + LR of each row from the per-pixel results (the census rowfin)
+            const int fd = sgm::ocv_vwta_dir(ndir);
+            uint64_t* res = (uint64_t*)(ws + l.ores);
+            rec.begin("ocv_paths", 2 * cells * (ndir - 1) + es * cells * (ndir - 1));
+            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st, fd), "ocv_paths");
+            rec.begin("ocv_vwta", 2 * cells + es * cells * (ndir - 1) + 8 * WH);
+            HIP_TRY(sgm::launch_ocv_vwta(A, B, V, ncells, ndir, gg, res, st), "ocv_vwta");
+            sgm::WtaFrames wf{};
+            wf.res[0] = res; wf.out[0] = dst; wf.n = 1;
+            rec.begin("ocv_rowfin", 8 * WH + 2 * WH);
+            HIP_TRY(sgm::launch_census_rowfin(wf, g, dst_stride, st), "ocv_rowfin");
+        } else {
+            rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
+            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
+            rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
+            HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
+        }
     }
     int rc = run_post(h, l, g, dOut, out_stride, rec);
     if (rc) return rc;
