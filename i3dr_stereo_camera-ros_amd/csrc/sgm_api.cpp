@@ -528,9 +528,10 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
             // disp2 + LR of each row from the per-pixel results (the census rowfin)
             const int fd = sgm::ocv_vwta_dir(ndir);
             uint64_t* res = (uint64_t*)(ws + l.ores);
-            rec.begin("ocv_paths", 2 * cells * (ndir - 1) + es * cells * (ndir - 1));
+            // the unfused stages' byte basis (C' counted once, in the paths stage)
+            rec.begin("ocv_paths", 2 * cells + es * cells * (ndir - 1));
             HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st, fd), "ocv_paths");
-            rec.begin("ocv_vwta", 2 * cells + es * cells * (ndir - 1) + 8 * WH);
+            rec.begin("ocv_vwta", es * cells * (ndir - 1) + 8 * WH);
             HIP_TRY(sgm::launch_ocv_vwta(A, B, V, ncells, ndir, gg, res, st), "ocv_vwta");
             sgm::WtaFrames wf{};
             wf.res[0] = res; wf.out[0] = dst; wf.n = 1;
