@@ -30,6 +30,9 @@ constexpr int kMaxCost = 32767;
 #ifndef SGM_OCV_PRIO
 #define SGM_OCV_PRIO 0     // longest-remaining-first wave priority (lr_prio) in k_ocv_paths
 #endif
+#ifndef SGM_OCV_VWTA_THR
+#define SGM_OCV_VWTA_THR 0   // k_ocv_vwta: uniqueness as one threshold per pixel (A/B knob)
+#endif
 #ifndef SGM_OCV_VWTA_PF
 #define SGM_OCV_VWTA_PF 3    // steps whose operands k_ocv_vwta keeps in flight (DPL <= 8)
 #endif
@@ -1030,12 +1033,35 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
         const int kmin = __builtin_amdgcn_readfirstlane(line_min_i32<LPL>(km));
         const int best = wta_untie(kmin & 2047, lanetie, 11);
         const int minS = (kmin >> 11) - 32768;
+#if SGM_OCV_VWTA_THR
+        // uniqueness: S * (100 - u) < minS * 100 is S < T = ceil(minS * 100 / (100 - u)) for
+        // u < 100 (one uniform threshold instead of a multiply per value)
+        bool hit = false;
+        if (g.uniq < 100) {
+            const int M = minS * 100, kq = 100 - g.uniq;
+            int T = (int)__builtin_ceilf((float)M / (float)kq);
+            T -= (T - 1) * kq >= M ? 1 : 0;
+            T += T * kq < M ? 1 : 0;
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                const int d = p * DPL + k;
+                hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] < T;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                const int d = p * DPL + k;
+                hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
+            }
+        }
+#else
         bool hit = false;
 #pragma unroll
         for (int k = 0; k < DPL; k++) {
             const int d = p * DPL + k;
             hit |= lane_act && d < g.D && (unsigned)(d - best + 1) > 2u && S[k] * (100 - g.uniq) < minS * 100;
         }
+#endif
         // every S saturated at MAX_COST: bestDisp stays -1 in OpenCV (see k_ocv_wta16)
         const bool rej = __ballot(hit) != 0ull || minS >= 32767;
         auto s_at = [&](int d) {                       // S[d] of the pixel (d wave-uniform)
