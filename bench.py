@@ -1,7 +1,14 @@
 """Benchmark of the MI355X-native SGM hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--config c3|c2|c5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+`--gpus N` alone (no WORLD_SIZE in the environment) starts the N rank processes itself, before
+this process makes any GPU call (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 set for each), and exits with the first failing rank's code; it exits
+non-zero if fewer than N devices are visible. Under torchrun the ranks come from the
+environment and WORLD_SIZE must equal --gpus. `--dry-run` runs the same rank logic with gloo
+and no HIP (a stand-in sleep per frame) for the CPU tests.
 
 Workload (BASELINE.json configs[2], the config the metric is quoted on): 1920x1080 stereo
 pairs, D = 256, 9x7 census + Hamming cost, 8-path SGM, WTA + uniqueness + subpixel +
@@ -13,10 +20,19 @@ only collectives are the timing barrier and the max-over-ranks reduction.
 `roofline` is the dominant kernel (algorithmic bytes / its average HIP-event duration over
 the timed region); `pipeline` is the whole frame (SURVEY §8d B_alg / per-frame device
 time). `cpu_baseline` times the CPU port (oracle) on a bounded sample on rank 0 at N = 1.
+
+C5 (BASELINE configs[4], 4096x3000 D=512, one frame): `--config c5` times it on its own — at
+N = 1 the single-device full frame (sgm_match_device), at N > 1 the overlap tile mode
+(sgm_match_tiled_device: N row bands + 128-row halos, one band per GPU, rows moved over xGMI)
+driven by one process (rank 0 under torchrun, the other ranks wait at a barrier) — and reports
+the disagreement with the 1-GPU full frame. The default C3 run adds the same measurement as
+its `c5` block (a child process after the C3 timed region, while the other ranks wait).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,7 +47,13 @@ CONFIGS = {
                subpixel=1, lr_check=1),
     "c2": dict(name="C2: 1920x1080 D=128 census9x7 8-path SGM (no subpixel / LR)", w=1920, h=1080, D=128,
                subpixel=0, lr_check=0),
+    "c5": dict(name="C5: 4096x3000 D=512 census9x7 8-path SGM + subpixel + LR-check, one frame (N > 1: row-band "
+                    "overlap tiles, one band per GPU, 128-row halos)", w=4096, h=3000, D=512, subpixel=1, lr_check=1),
 }
+C5_HALO = 128           # overlap mode, 0 disagreement at C5 with 128-row halos
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+            "TORCHELASTIC_MAX_RESTARTS", "GROUP_WORLD_SIZE")
 
 
 def shard_frames(n_frames_per_rank, rank, seed0=0):
@@ -197,6 +219,186 @@ def c1_reference_matcher(orc, synth, reps=20):
             "bit_exact": bool(np.array_equal(got, ref))}
 
 
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices():
+    """HIP devices this process may use; torch.cuda.device_count() does not initialise the GPU
+    on this image, so it is safe before the rank processes are started."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(n, argv, dry_run=False):
+    """`bench.py --gpus N` without WORLD_SIZE: one child process per rank (this process never
+    touches the GPU), the torchrun environment set for each. Returns the exit code: 0 if every
+    rank succeeded, else the first failing rank's code (the others are terminated)."""
+    if not dry_run:
+        vis = visible_devices()
+        if vis < n:
+            print(f"bench.py: --gpus {n} but only {vis} HIP device(s) visible", file=sys.stderr)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = {k: v for k, v in os.environ.items() if k not in RANK_ENV}
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_step(rank, n_frames):
+    """--dry-run stand-in for one step of a rank (no HIP): rank r takes (1 + r) ms per frame,
+    so the ranks finish at different times and the MAX reduction is visible."""
+    time.sleep(1e-3 * (1 + rank) * n_frames)
+
+
+def c5_frame_ms(pkg, torch, eng, dl, dr, out, W, H, devices, steps, warmup, stream, tstream):
+    """ms per C5 frame over `steps` timed frames: the full frame on one device, or the overlap
+    tile mode over `devices` (one band each), inputs resident in HBM of the engine's device."""
+    if len(devices) == 1:
+        run = lambda: eng.match_device(dl.data_ptr(), dr.data_ptr(), W, H, W, out.data_ptr(), W, stream)
+    else:
+        run = lambda: eng.match_tiled_device(dl.data_ptr(), dr.data_ptr(), W, H, W, out.data_ptr(), W, len(devices),
+                                             C5_HALO, devices=devices, stream=stream)
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    tstream.synchronize()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps
+
+
+def run_c5(args, n_gpus, pkg, torch, device):
+    """C5 on one process driving devices 0..n_gpus-1 (see the module docstring)."""
+    cfg = CONFIGS["c5"]
+    W, H, D = cfg["w"], cfg["h"], cfg["D"]
+    synth = __import__("__graft_entry__")._load_file("sgm_synth", os.path.join(ROOT, "i3dr_stereo_camera-ros_amd",
+                                                                                "synth.py"))
+    left, right, _ = synth.stereo_pair(H, W, 0, D, seed=5, with_truth=False)
+    params = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=0, p1=10, p2=120,
+                                uniqueness_ratio=5, subpixel=1, lr_check=1, disp12_max_diff=1, median=0,
+                                speckle_window_size=0)
+    eng = pkg.Engine(device, params)
+    dl, dr = torch.from_numpy(left).to(device), torch.from_numpy(right).to(device)
+    out = torch.empty((H, W), dtype=torch.int16, device=device)
+    tstream = torch.cuda.Stream(device)
+    stream = tstream.cuda_stream
+    devices = list(range(n_gpus))
+    ms = c5_frame_ms(pkg, torch, eng, dl, dr, out, W, H, devices, args.steps, args.warmup, stream, tstream)
+    res = {"workload": cfg["name"], "width": W, "height": H, "num_disparities": D, "n_gpus": n_gpus,
+           "ms_per_frame": round(ms, 4), "pairs_per_s": round(1000.0 / ms, 3), "frames_timed": args.steps,
+           "mode": "full frame, sgm_match_device" if n_gpus == 1 else
+                   f"overlap tiles: {n_gpus} row bands + {C5_HALO}-row halos, sgm_match_tiled_device "
+                   f"(one band per GPU, host thread + stream per device, rows over xGMI)"}
+    b_alg = algorithmic_bytes(W, H, D)
+    res["roofline"] = {"bound": "hbm", "B_alg_per_frame": b_alg, "achieved": round(b_alg / (ms * 1e-3) / 1e9, 1),
+                       "peak": HBM_PEAK_GBS * n_gpus, "unit": "GB/s",
+                       "frac": round(b_alg / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * n_gpus), 4),
+                       "basis": "SURVEY 8d B_alg of one C5 frame over the frame time, against N x 8 TB/s"}
+    if n_gpus == 1:
+        eng.set_profiling(True)
+        eng.match_device(dl.data_ptr(), dr.data_ptr(), W, H, W, out.data_ptr(), W, stream)
+        tstream.synchronize()
+        res["stages"] = {n: round(t, 4) for n, t, _ in eng.stage_times()}
+        eng.set_profiling(False)
+        res["disagreement_vs_full_frame"] = 0.0
+    else:
+        tiled = out.cpu().numpy()
+        eng.match_device(dl.data_ptr(), dr.data_ptr(), W, H, W, out.data_ptr(), W, stream)
+        tstream.synchronize()
+        full = out.cpu().numpy()
+        res["disagreement_vs_full_frame"] = float((tiled != full).mean())
+    eng.close()
+    return res
+
+
+def c5_leg(args, world):
+    """The default run's `c5` block: bench.py --config c5 in a child process (own HIP context,
+    a fault there cannot take the C3 line with it), over the same number of GPUs."""
+    env = {k: v for k, v in os.environ.items() if k not in RANK_ENV}
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", "c5", "--gpus", str(world), "--steps",
+           str(args.c5_frames), "--warmup", "1", "--no-cpu-baseline", "--c5-only"]
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.c5_timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {args.c5_timeout} s"}
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}: {p.stderr.strip()[-400:]}"}
+    return json.loads(lines[-1])
+
+
+def gather_shard(seeds, elapsed, distributed, busy=None):
+    """Per-rank record of the frame shard: the synthetic frame seeds each rank owned and its own
+    timed-region length (the line's value uses the MAX of these)."""
+    mine = {"seeds": list(seeds), "elapsed_s": round(elapsed, 6)}
+    if busy is not None:
+        mine["busy_s"] = round(busy, 6)
+    if not distributed:
+        return [mine]
+    import torch.distributed as dist
+    objs = [None] * dist.get_world_size()
+    dist.all_gather_object(objs, mine)
+    return objs
+
+
+def dry_main(args, world, rank):
+    """--dry-run: the rank / shard / timing logic of main() with gloo and no HIP."""
+    import torch.distributed as dist
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("gloo")
+    ids = shard_frames(args.distinct, rank)
+    for _ in range(args.warmup):
+        dry_step(rank, 1)
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dry_step(rank, 1)
+    busy = time.perf_counter() - t0        # this rank's own work, before the closing barrier
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = max_over_ranks(elapsed)
+    shard = gather_shard(ids, elapsed, distributed, busy)
+    if rank == 0:
+        frames_total = args.frames * args.steps * world
+        print(json.dumps({"metric": METRIC, "value": round(frames_total / elapsed_max, 3), "unit": "pairs/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "dry run (no HIP work)",
+                          "elapsed_max_s": elapsed_max, "shard": shard,
+                          "config": {"workload": "dry run", "parallelism": f"frame-shard x{world}"}}))
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,7 +414,28 @@ def main():
     ap.add_argument("--host-io", action="store_true",
                     help="host buffers in and out (sgm_match_batch: pinned rings, H2D/D2H overlapped with the "
                          "kernels); PCIe-inclusive, reported beside the device-resident value, never as it")
+    ap.add_argument("--dry-run", action="store_true", help="rank logic only: gloo, no HIP (CPU tests)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the default run's C5 block")
+    ap.add_argument("--c5-frames", type=int, default=10, help="timed C5 frames of the default run's c5 block")
+    ap.add_argument("--c5-timeout", type=int, default=300)
+    ap.add_argument("--c5-only", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    # --gpus N without a torchrun environment: start the N ranks here, before any GPU call
+    # (C5 is one process driving every device, so it needs no rank processes)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.config != "c5":
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_run))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: n_gpus must equal --gpus", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_main(args, world, rank)
     cfg = CONFIGS[args.config]
 
     import numpy as np
@@ -220,18 +443,44 @@ def main():
     import torch.distributed as dist
     import __graft_entry__ as ge
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    n_vis = torch.cuda.device_count()
+    need = max(world, args.gpus if args.config == "c5" else 1)
+    if n_vis < need or local_rank >= n_vis:
+        print(f"bench.py: needs {need} HIP device(s) (rank {rank}, local rank {local_rank}), {n_vis} visible",
+              file=sys.stderr)
+        sys.exit(2)
     if distributed:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
-
     pkg = ge.load_package()
+
+    if args.config == "c5":
+        c5 = None
+        if rank == 0:
+            c5 = run_c5(args, max(world, args.gpus), pkg, torch, device)
+        if distributed:
+            dist.barrier()
+        if rank == 0:
+            if args.c5_only:
+                print(json.dumps(c5))
+            else:
+                res = {"metric": METRIC, "value": c5["pairs_per_s"], "unit": "pairs/s", "n_gpus": c5["n_gpus"],
+                       "steps": args.steps, "warmup": args.warmup, "ms_per_step": c5["ms_per_frame"],
+                       "ms_per_frame": c5["ms_per_frame"], "higher_is_better": True, "scaling": "strong",
+                       "vs_baseline": None, "dtype": "u8", "data": "synthetic (numpy PCG64 textured pair, resident in HBM)",
+                       "config": {"workload": c5["workload"], "width": c5["width"], "height": c5["height"],
+                                  "num_disparities": c5["num_disparities"],
+                                  "parallelism": "single device" if c5["n_gpus"] == 1 else f"row-band tiles x{c5['n_gpus']}"},
+                       "roofline": c5["roofline"], "c5": c5}
+                print(json.dumps(res))
+        if distributed:
+            dist.destroy_process_group()
+        return
+
     synth = ge._load_file("sgm_synth", os.path.join(ge.PKG_DIR, "synth.py"))
     W, H, D = cfg["w"], cfg["h"], cfg["D"]
     params = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, min_disparity=0, p1=10, p2=120,
@@ -301,6 +550,7 @@ def main():
     eng.set_profiling(False)
 
     elapsed_max = max_over_ranks(elapsed, device)
+    shard = gather_shard(ids, elapsed, distributed)
 
     # single-frame latency beside the batch throughput (BASELINE's C2 is quoted as a single
     # frame): one sgm_match_device per frame on resident buffers, HIP events on the stream
@@ -391,13 +641,17 @@ def main():
                         "GBps": round(b / (ms * 1e-3) / 1e9, 1)} for n, ms, b in stages],
             "profiled_frames": n_prof,
             "single_frame": single,
+            "shard": shard,
         }
+    eng.close()
+    if rank == 0:
+        if args.config == "c3" and not args.no_c5 and not args.host_io and not args.rectify:
+            res["c5"] = c5_leg(args, world)          # the other ranks wait at the barrier below
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(res))
-    eng.close()
     if distributed:
-        dist.barrier()              # rank 0's single-frame / CPU legs end before the group does
+        dist.barrier()              # rank 0's single-frame / C5 / CPU legs end before the group does
         dist.destroy_process_group()
 
 

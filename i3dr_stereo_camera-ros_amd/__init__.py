@@ -24,6 +24,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsgm_hip.so")
 
+ABI_VERSION = 4     # include/sgm_hip.h SGM_ABI_VERSION
 MODE_OCV_SGBM5 = 0
 MODE_OCV_HH8 = 1
 MODE_CENSUS8 = 2
@@ -56,7 +57,7 @@ def ocv_compat_from_env(default=COMPAT_MELODIC):
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
     "sgm_check_params", "sgm_match", "sgm_match_f32", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
-    "sgm_match_tiled_exact", "sgm_synchronize", "sgm_last_error",
+    "sgm_match_tiled_device", "sgm_match_tiled_exact", "sgm_abi_version", "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
     "sgm_remap_cubic", "sgm_cubic_table", "sgm_set_rectification", "sgm_match_device_batch_rect", "sgm_debug_census",
@@ -120,7 +121,12 @@ def load_library(path=None):
     L.sgm_match_device_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, vp]
     L.sgm_match_batch.argtypes = [vp, P(vp), P(vp), ci, ci, ci, sz, P(vp), sz, P(ci), ci]
     L.sgm_match_tiled.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, ci, P(ci), ci]
+    L.sgm_match_tiled_device.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, ci, P(ci), ci, vp]
     L.sgm_match_tiled_exact.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, P(ci), ci]
+    L.sgm_abi_version.restype = ci
+    if L.sgm_abi_version() != ABI_VERSION:
+        raise ImportError(f"{path}: C-ABI version {L.sgm_abi_version()} != {ABI_VERSION} (include/sgm_hip.h "
+                          "SGM_ABI_VERSION): rebuild the library")
     L.sgm_synchronize.argtypes = [vp]
     L.sgm_last_error.argtypes = [vp]
     L.sgm_last_error.restype = ctypes.c_char_p
@@ -345,6 +351,18 @@ class Engine:
         self._check(self.lib.sgm_match_tiled(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w, n_bands, halo,
                                              devs, nd))
         return out
+
+    def match_tiled_device(self, d_left, d_right, width, height, stride, d_out, out_stride, n_bands, halo,
+                           devices=None, stream=None):
+        """Overlap tile mode on device buffers of this engine's device (C5 frame resident in
+        HBM): band b runs on devices[b % len(devices)], rows moved by peer copies."""
+        if devices:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            nd = len(devices)
+        else:
+            devs, nd = None, 0
+        self._check(self.lib.sgm_match_tiled_device(self.h, d_left, d_right, width, height, stride, d_out, out_stride,
+                                                    n_bands, halo, devs, nd, stream))
 
     def match_tiled_exact(self, left, right, n_bands, devices=None):
         """One frame split into row bands over the devices, exact mode: the

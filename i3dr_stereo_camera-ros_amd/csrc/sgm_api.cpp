@@ -929,6 +929,8 @@ int sgm_get_params(const sgm_handle* h, sgm_params* p)
     return SGM_OK;
 }
 
+int sgm_abi_version(void) { return SGM_ABI_VERSION; }
+
 int sgm_check_params(const sgm_params* p, int width, int height)
 {
     if (!p) return SGM_ERR_ARG;
@@ -1543,6 +1545,80 @@ int sgm_match_tiled(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
 
 }  // extern "C"
 
+static void enable_peer_pair(int a, int b);
+
+// Overlap tile mode on device buffers (the C5 frame already in HBM of h's device): band b's
+// rows + halo go device -> devices[b % n] (xGMI peer copy), are matched there by
+// sgm_match_device on that device's sub-handle, and the band's own rows come back into
+// d_disp. Each device's bands run on its own host thread and stream.
+static int tiled_copy(void* dst, int ddev, size_t dpitch, const void* src, int sdev, size_t spitch, size_t width,
+                      size_t rows, hipStream_t st)
+{
+    if (ddev == sdev || (dpitch == width && spitch == width)) {
+        const hipError_t e = ddev == sdev ? hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows,
+                                                             hipMemcpyDeviceToDevice, st)
+                                          : hipMemcpyPeerAsync(dst, ddev, src, sdev, width * rows, st);
+        return e == hipSuccess ? 0 : (int)e;
+    }
+    for (size_t r = 0; r < rows; r++) {       // strided rows across devices: one peer copy per row
+        const hipError_t e = hipMemcpyPeerAsync((char*)dst + r * dpitch, ddev, (const char*)src + r * spitch, sdev,
+                                                width, st);
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+extern "C" int sgm_match_tiled_device(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, int H,
+                                      size_t stride, int16_t* dOut, size_t out_stride, int n_bands, int halo,
+                                      const int* devices, int n_dev, void* stream)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!dL || !dR || !dOut || W <= 0 || H <= 0 || stride < (size_t)W || out_stride < (size_t)W || n_bands < 1 ||
+        halo < 0)
+        return fail(h, SGM_ERR_ARG, "bad buffers, sizes, band count or halo");
+    if (h->rect_on) return fail(h, SGM_ERR_UNSUPPORTED, "the tile mode takes rectified images");
+    n_bands = std::min(n_bands, H);
+    std::vector<int> devs;
+    int rc = open_subs(h, devices, n_dev, devs);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if ((rc = ensure_stream(h))) return rc;
+        if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize caller");
+        if (h->done_stream) HIP_TRY(hipEventSynchronize(h->done), "hipEventSynchronize");
+    }
+    for (int d : devs) enable_peer_pair(d, h->device);
+    const int nd = (int)devs.size(), hdev = h->device;
+    return run_on_subs(h, devs, [&](int t, sgm_handle* sub) {
+        for (int b = t; b < n_bands; b += nd) {
+            const int c0 = (int)((long long)b * H / n_bands), c1 = (int)((long long)(b + 1) * H / n_bands);
+            const int e0 = std::max(0, c0 - halo), e1 = std::min(H, c1 + halo), He = e1 - e0;
+            const size_t img = align_up((size_t)W * He), need = 2 * img + (size_t)W * He * 2;
+            int r = ensure_stream(sub);
+            if (r) return r;
+            if (sub->io_dev_size < need) {
+                (void)hipStreamSynchronize(sub->stream);
+                if (sub->io_dev) { (void)hipFree(sub->io_dev); sub->io_dev = nullptr; sub->io_dev_size = 0; }
+                if (hipMalloc(&sub->io_dev, need) != hipSuccess)
+                    return fail(sub, SGM_ERR_ALLOC, "hipMalloc band buffers");
+                sub->io_dev_size = need;
+            }
+            uint8_t* bl = (uint8_t*)sub->io_dev;
+            uint8_t* br = bl + img;
+            int16_t* bo = (int16_t*)(br + img);
+            if ((r = tiled_copy(bl, sub->device, W, dL + (size_t)e0 * stride, hdev, stride, W, He, sub->stream)) ||
+                (r = tiled_copy(br, sub->device, W, dR + (size_t)e0 * stride, hdev, stride, W, He, sub->stream)))
+                return fail(sub, SGM_ERR_DEVICE, std::string("band input copy: ") + hipGetErrorString((hipError_t)r));
+            if ((r = sgm_match_device(sub, bl, br, W, He, W, bo, W, nullptr))) return r;
+            if ((r = tiled_copy(dOut + (size_t)c0 * out_stride, hdev, out_stride * 2, bo + (size_t)(c0 - e0) * W,
+                                sub->device, (size_t)W * 2, (size_t)W * 2, c1 - c0, sub->stream)))
+                return fail(sub, SGM_ERR_DEVICE, std::string("band output copy: ") + hipGetErrorString((hipError_t)r));
+            if (hipStreamSynchronize(sub->stream) != hipSuccess) return fail(sub, SGM_ERR_DEVICE, "band stream");
+        }
+        return (int)SGM_OK;
+    });
+}
+
 // ------------------------------------------------------------------ exact tile mode ----
 // SURVEY §8(e) "single huge frame", exact mode. Band b (rows [c0, c1)) runs on its own
 // handle: census of its rows (+3 image rows of halo, so the codes equal the full frame's),
@@ -1864,6 +1940,8 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
 }
 
 }  // namespace
+
+static void enable_peer_pair(int a, int b) { enable_peer(a, b); enable_peer(b, a); }
 
 extern "C" {
 

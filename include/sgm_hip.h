@@ -31,6 +31,15 @@
 extern "C" {
 #endif
 
+/* ---- ABI version ------------------------------------------------------------------- */
+/* Bumped whenever a struct or signature of this header changes. Round 3 grew sgm_params
+ * from 14 to 15 ints (ocv_compat, version 3); round 4 added sgm_match_tiled_device
+ * (version 4). A caller compiled against an older header must check sgm_abi_version()
+ * == SGM_ABI_VERSION before passing an sgm_params (a 14-int struct would be read one int
+ * past its end).                                                                         */
+#define SGM_ABI_VERSION 4
+int  sgm_abi_version(void);
+
 /* ---- status codes ------------------------------------------------------------------ */
 #define SGM_OK                0
 #define SGM_ERR_ARG          -1   /* null pointer, bad size / stride                      */
@@ -158,6 +167,16 @@ int  sgm_match_batch(sgm_handle* h, const uint8_t* const* lefts, const uint8_t* 
 int  sgm_match_tiled(sgm_handle* h, const uint8_t* left, const uint8_t* right, int width, int height,
                      size_t stride, int16_t* disp, size_t out_stride, int n_bands, int halo,
                      const int* devices, int n_dev);
+
+/* Overlap mode on device buffers (C5 with the frame already in HBM of h's device): band b's
+ * rows + halo are copied to devices[b % n_dev] (hipMemcpyPeerAsync over xGMI when the device
+ * differs), matched there with sgm_match_device on that device's sub-handle, and the band's
+ * own rows are copied back into d_disp. One host thread + stream per device. Work queued on
+ * `stream` (may be NULL) before the call is complete before the band copies start;
+ * synchronous: d_disp is complete on return. Same results as sgm_match_tiled.             */
+int  sgm_match_tiled_device(sgm_handle* h, const uint8_t* d_left, const uint8_t* d_right, int width, int height,
+                            size_t stride, int16_t* d_disp, size_t out_stride, int n_bands, int halo,
+                            const int* devices, int n_dev, void* stream);
 
 /* The same band split in exact mode (SURVEY §8(e) "exact mode", census mode only): band b
  * continues the path lines of its neighbours. Its downward sweeps start from the last

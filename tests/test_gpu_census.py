@@ -289,6 +289,51 @@ def test_c5_tiled_vs_full_frame(engine, synth, pkg):
     assert (full != -16).mean() > 0.5
 
 
+@pytest.mark.parametrize("bands,halo,n_dev,pad", [(1, 0, 1, 0), (3, 16, 2, 0), (4, 64, 4, 13), (5, 200, 3, 7)])
+def test_tiled_device_equals_host_tiles(engine, oracle, synth, pkg, bands, halo, n_dev, pad):
+    """sgm_match_tiled_device (device buffers, band b on devices[b % n], here all device 0 as
+    bench.py --config c5 runs it with N bands on one GPU) is band for band the oracle on the
+    band's extended rows, i.e. the host overlap mode; strided input / output rows included."""
+    import torch
+    h, w, D = 200, 320, 96
+    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=47 + bands)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, median=1, speckle_window_size=20, speckle_range=2)
+    engine.set_params(p)
+    s_in, s_out = w + pad, w + 2 * pad
+    dl = torch.zeros((h, s_in), dtype=torch.uint8, device="cuda")
+    dr = torch.zeros((h, s_in), dtype=torch.uint8, device="cuda")
+    dl[:, :w] = torch.from_numpy(left).cuda()
+    dr[:, :w] = torch.from_numpy(right).cuda()
+    out = torch.full((h, s_out), 1234, dtype=torch.int16, device="cuda")
+    engine.match_tiled_device(dl.data_ptr(), dr.data_ptr(), w, h, s_in, out.data_ptr(), s_out, bands, halo,
+                              devices=[0] * n_dev)
+    got = out.cpu().numpy()
+    assert (got[:, w:] == 1234).all()                       # row padding untouched
+    got = got[:, :w]
+    assert np.array_equal(got, engine.match_tiled(left, right, bands, halo))
+    op = to_oracle_params(oracle, p)
+    for b in range(bands):
+        c0, c1 = b * h // bands, (b + 1) * h // bands
+        e0, e1 = max(0, c0 - halo), min(h, c1 + halo)
+        assert np.array_equal(got[c0:c1], oracle.match(op, left[e0:e1], right[e0:e1])[c0 - e0:c1 - e0]), f"band {b}"
+
+
+def test_bench_c5_block_on_one_device():
+    """bench.py --config c5 --gpus 1 (the driver's default run adds the same block): the full
+    frame on one device, with its roofline and stage split."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", "c5", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["n_gpus"] == 1 and res["c5"]["disagreement_vs_full_frame"] == 0.0
+    assert 0.2 < res["roofline"]["frac"] < 1.0 and "paths8" in " ".join(res["c5"]["stages"])
+
+
 EXACT_CASES = [
     (dict(num_disparities=64), 2),
     (dict(num_disparities=64), 5),
