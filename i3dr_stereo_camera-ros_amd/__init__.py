@@ -48,11 +48,17 @@ COMPAT_NAMES = {"scalar": COMPAT_SCALAR, "noetic": COMPAT_NOETIC, "melodic": COM
 def ocv_compat_from_env(default=COMPAT_MELODIC):
     """SGM_HIP_OCV_COMPAT = melodic | noetic | scalar | <bits> (the adapters read the same
     variable)."""
-    v = os.environ.get("SGM_HIP_OCV_COMPAT")
+    raw = os.environ.get("SGM_HIP_OCV_COMPAT")
+    v = (raw or "").strip().lower()
     if not v:
         return default
-    v = v.strip().lower()
-    return COMPAT_NAMES[v] if v in COMPAT_NAMES else int(v, 0) & 7
+    if v in COMPAT_NAMES:
+        return COMPAT_NAMES[v]
+    try:
+        return int(v, 0) & 7
+    except ValueError:      # the C++ adapter core (hip_sgm_core.cpp) warns and keeps the default too
+        sys.stderr.write(f'SGM_HIP_OCV_COMPAT="{raw}" is not melodic | noetic | scalar | <bits>: using {default}\n')
+        return default
 
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",

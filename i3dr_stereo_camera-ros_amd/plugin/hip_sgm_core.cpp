@@ -1,22 +1,40 @@
 // hip_sgm_core.cpp — see hip_sgm_core.h.
 #include "hip_sgm_core.h"
 
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <string>
 
 namespace sgm_hip {
 
 // SGM_HIP_OCV_COMPAT = melodic | noetic | scalar | <bits>: the OpenCV build the OCV modes
 // reproduce (include/sgm_hip.h SGM_OCV_*); unset: sgm_default_params' melodic default.
+// Case and surrounding blanks are ignored; an unparseable value warns on stderr and keeps
+// the fallback (the Python mirror's ocv_compat_from_env does the same).
 int ocv_compat_from_env(int fallback)
 {
     const char* e = std::getenv("SGM_HIP_OCV_COMPAT");
-    if (!e || !*e) return fallback;
-    if (!std::strcmp(e, "melodic")) return SGM_OCV_COMPAT_MELODIC;
-    if (!std::strcmp(e, "noetic")) return SGM_OCV_COMPAT_NOETIC;
-    if (!std::strcmp(e, "scalar")) return SGM_OCV_COMPAT_SCALAR;
-    return (int)std::strtol(e, nullptr, 0) & (SGM_OCV_COL0_LEGACY | SGM_OCV_SIMD_SAT | SGM_OCV_LANE_TIE);
+    if (!e) return fallback;
+    std::string v(e);
+    while (!v.empty() && std::isspace((unsigned char)v.back())) v.pop_back();
+    size_t b = 0;
+    while (b < v.size() && std::isspace((unsigned char)v[b])) b++;
+    v = v.substr(b);
+    if (v.empty()) return fallback;
+    for (char& c : v) c = (char)std::tolower((unsigned char)c);
+    if (v == "melodic") return SGM_OCV_COMPAT_MELODIC;
+    if (v == "noetic") return SGM_OCV_COMPAT_NOETIC;
+    if (v == "scalar") return SGM_OCV_COMPAT_SCALAR;
+    char* end = nullptr;
+    const long bits = std::strtol(v.c_str(), &end, 0);
+    if (end == v.c_str() || *end) {
+        std::cerr << "SGM_HIP_OCV_COMPAT=\"" << e << "\" is not melodic | noetic | scalar | <bits>: using "
+                  << fallback << std::endl;
+        return fallback;
+    }
+    return (int)bits & (SGM_OCV_COL0_LEGACY | SGM_OCV_SIMD_SAT | SGM_OCV_LANE_TIE);
 }
 
 MatcherCore::MatcherCore(int device, int mode) : device_(device)

@@ -41,6 +41,10 @@ int main(int argc, char** argv)
         std::printf("setters ok\n");
         return 0;
     }
+    if (!std::strcmp(mode, "compat")) {          // SGM_HIP_OCV_COMPAT as the adapter core reads it
+        std::printf("%d\n", sgm_hip::ocv_compat_from_env(SGM_OCV_COMPAT_MELODIC));
+        return 0;
+    }
     if (!std::strcmp(mode, "init")) {
         sgm_hip::MatcherCore m(0, SGM_MODE_OCV_SGBM5);
         m.setDisparityRange(16, 10);

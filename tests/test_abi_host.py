@@ -53,16 +53,21 @@ def test_default_params_match_node_defaults(pkg):
 
 
 @pytest.mark.parametrize("val,bits", [(None, 7), ("melodic", 7), ("noetic", 2), ("scalar", 0), ("5", 5),
-                                      ("0x3", 3)])
+                                      ("0x3", 3), ("Melodic", 7), (" melodic ", 7), ("NOETIC\t", 2), ("", 7),
+                                      ("melodik", 7), ("3x", 7), ("  ", 7)])
 def test_ocv_compat_env(pkg, monkeypatch, val, bits):
     """SGM_HIP_OCV_COMPAT selects the OpenCV build, in the Python mirror's
-    MatcherHIPSGM like in the C++ adapter core."""
+    MatcherHIPSGM and in the C++ adapter core alike: case and blanks ignored, an unparseable
+    value warns and keeps the melodic default."""
     if val is None:
         monkeypatch.delenv("SGM_HIP_OCV_COMPAT", raising=False)
     else:
         monkeypatch.setenv("SGM_HIP_OCV_COMPAT", val)
     assert pkg.ocv_compat_from_env() == bits
     assert pkg.MatcherHIPSGM(" ", (0, 0), mode=pkg.MODE_OCV_SGBM5).params.ocv_compat == bits
+    exe = os.path.join(ROOT, "i3dr_stereo_camera-ros_amd", "lib", "plugin_core_test")
+    r = subprocess.run([exe, "compat"], capture_output=True, text=True)
+    assert r.returncode == 0 and int(r.stdout) == bits, r.stderr
 
 
 @pytest.mark.parametrize("mode,D,expect", [("census", 64, 0), ("census", 24, -2), ("census", 0, -2),
