@@ -63,7 +63,7 @@ def ocv_compat_from_env(default=COMPAT_MELODIC):
 EXPORTS = [
     "sgm_device_count", "sgm_create", "sgm_destroy", "sgm_default_params", "sgm_set_params", "sgm_get_params",
     "sgm_check_params", "sgm_match", "sgm_match_f32", "sgm_match_device", "sgm_match_device_batch", "sgm_match_batch", "sgm_match_tiled",
-    "sgm_match_tiled_device", "sgm_match_tiled_exact", "sgm_abi_version", "sgm_synchronize", "sgm_last_error",
+    "sgm_match_tiled_device", "sgm_match_tiled_exact", "sgm_abi_version", "sgm_host_register", "sgm_host_unregister", "sgm_synchronize", "sgm_last_error",
     "sgm_set_profiling", "sgm_get_stage_times", "sgm_profiled_matches", "sgm_stage_name", "sgm_stage_bytes",
     "sgm_stage_launches", "sgm_disparity_to_msg", "sgm_calc_q", "sgm_depth_points", "sgm_rectify_map",
     "sgm_remap_cubic", "sgm_cubic_table", "sgm_set_rectification", "sgm_match_device_batch_rect", "sgm_debug_census",
@@ -130,6 +130,8 @@ def load_library(path=None):
     L.sgm_match_tiled_device.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, ci, P(ci), ci, vp]
     L.sgm_match_tiled_exact.argtypes = [vp, vp, vp, ci, ci, sz, vp, sz, ci, P(ci), ci]
     L.sgm_abi_version.restype = ci
+    L.sgm_host_register.argtypes = [vp, vp, sz]
+    L.sgm_host_unregister.argtypes = [vp, vp]
     if L.sgm_abi_version() != ABI_VERSION:
         raise ImportError(f"{path}: C-ABI version {L.sgm_abi_version()} != {ABI_VERSION} (include/sgm_hip.h "
                           "SGM_ABI_VERSION): rebuild the library")
@@ -357,6 +359,13 @@ class Engine:
         self._check(self.lib.sgm_match_tiled(self.h, _ptr(left), _ptr(right), w, h, w, _ptr(out), w, n_bands, halo,
                                              devs, nd))
         return out
+
+    def host_register(self, arr):
+        """Page-lock a host array (sgm_host_register): matches into it copy out asynchronously."""
+        self._check(self.lib.sgm_host_register(self.h, arr.ctypes.data, arr.nbytes))
+
+    def host_unregister(self, arr):
+        self._check(self.lib.sgm_host_unregister(self.h, arr.ctypes.data))
 
     def match_tiled_device(self, d_left, d_right, width, height, stride, d_out, out_stride, n_bands, halo,
                            devices=None, stream=None):

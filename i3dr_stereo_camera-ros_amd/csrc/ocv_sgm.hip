@@ -169,9 +169,11 @@ struct PixGeo {
 };
 __host__ inline size_t pix_lds_bytes(const Geom& g) { return PixGeo(g).bytes(); }
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+template <bool GATED>      // GATED: only for the flagged frames (the fused cost made C' for the others)
 __global__ __launch_bounds__(256) void k_ocv_pixhsum(const uint8_t* __restrict__ planes, Geom g,
                                                      int16_t* __restrict__ hs)
 {
+    if (GATED && !ocv_flagged(g)) return;
     extern __shared__ uint32_t lds_pix32[];
     const PixGeo pg(g);
     const int XB = pg.XB, DCmax = pg.DC, NX = pg.NX, M = pg.M, PP = pg.PP;
@@ -407,6 +409,315 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_sat(const int16_t* __restrict_
             c = g.P2;                                      // MODE_HH: never recomputed, the P2 init
         }                                                  // MODE_SGBM: the last computed row
         C[(size_t)y * rc + i] = (int16_t)c;
+    }
+}
+
+// Birchfield-Tomasi intervals of the four planes (left pf, left raw, right pf, right raw),
+// packed u | lo << 8 | hi << 16 per pixel: what every fused-cost block stages per row (one
+// dword load per entry instead of three byte loads and the min/max).
+__global__ __launch_bounds__(256) void k_ocv_btplanes(const uint8_t* __restrict__ planes, int W, int H,
+                                                      uint32_t* __restrict__ bt)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
+    if (x >= W) return;
+    int u, lo, hi;
+    bt_lohi(planes + (size_t)c * W * H + (size_t)y * W, x, W, u, lo, hi);
+    bt[((size_t)c * H + y) * W + x] = (uint32_t)u | (uint32_t)lo << 8 | (uint32_t)hi << 16;
+}
+
+// ---- the whole cost stage in one pass: pixel cost + vertical box + horizontal box + P2 ------
+// (replaces k_ocv_pixhsum + k_ocv_vsum_seg, whose 2 B/cell horizontal-sum volume went to HBM
+// and was read back twice: 1.71 GB moved for 0.50 GB of C' at 1080p D=128, PMC r03). The box
+// is separable and OpenCV's int16 wrap is arithmetic mod 2^16, so the vertical sums can come
+// first: a block owns a tile of XB output columns x DC disparities over a band of rows and walks
+// the band's rows (+ SH2 above and below) once. Per row:
+//   staging threads (waves 4-7): the BT intervals of the row (k_ocv_btplanes) into LDS in
+//       k_ocv_pixhsum's formats (left columns duplicated into both halves of a word, right
+//       entries as pair words of adjacent disparities);
+//   every thread: the pixel costs of its staged column k and I disparity pairs (packed u16 ops,
+//       the left words kept in registers), and its vertical window sums V: V += P - P(row - R),
+//       the last R = 2*SH2 + 1 rows of P in registers (the row loop is unrolled by R, so every
+//       ring slot is a static register); V of the row to LDS;
+//   box threads (waves 0-3): the horizontal box of the previous row's V (a sliding window per
+//       segment of output columns, staged columns outside [0, width1) read as the edge column:
+//       OpenCV's replicate rule), + P2, stored as int16 (u16 wrap = OpenCV's CostType store);
+// one barrier per row (staging, V and the box double-buffered). The true sums are exact in u16
+// when (2*SW2+1)(2*SH2+1)(2*ftzero+63) <= 65535 (the launcher's condition), so the overflow flag
+// of Geom::wide == 2 is max(box) > ovf_thr - P2, as k_ocv_vsum_seg computes it (no horizontal sum
+// can leave int16 under that bound). OpenCV's bottom-row rule: the band holding the last computed
+// row ylast = max(H - SH2 - 1, 0) also writes the rows below it (its last values in MODE_SGBM, P2
+// in MODE_HH); COL0_LEGACY's column is written by k_ocv_col0_legacy afterwards.
+// Block ids are dealt XCD-aware: the DC-chunks of one tile (and then the next strip of the band)
+// run back to back on one XCD, so the partial lines of their C' rows merge in that L2.
+constexpr int kFuseThreads = 512;
+constexpr int kFuseNX = 128;              // staged columns per block: 4 threads per column
+__host__ __device__ inline int fuse_xb(const Geom& g) { return kFuseNX - 2 * g.SW2; }
+struct FuseGeo {
+    int DC, M, MH;
+    __host__ __device__ FuseGeo(int dpc) {
+        DC = 2 * dpc;
+        M = ((kFuseNX + DC) & ~1) + 2;
+        MH = M / 2;
+    }
+    __host__ __device__ int stage_words() const { return 6 * kFuseNX + 7 * M; }
+    __host__ __device__ size_t lds_bytes(int dpc) const {
+        return (size_t)4 * (2 * stage_words() + 2 * kFuseNX * dpc);
+    }
+};
+struct FuseGrid {
+    int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
+};
+template <int R, int DPC, int I>
+__global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
+                                                                 FuseGrid fg, int16_t* __restrict__ C)
+{
+    static_assert(DPC / I * kFuseNX == kFuseThreads, "4 threads per staged column");
+    constexpr int TPC = DPC / I;
+    extern __shared__ uint32_t lds_fuse[];
+    const FuseGeo fz(DPC);
+    const int DC = fz.DC, M = fz.M, MH = fz.MH, NX = kFuseNX;
+    const int SW2 = g.SW2, SH2 = g.SH2, XB = NX - 2 * SW2;
+    // XCD-aware deal: XCD x = blockIdx.x % 8 runs logical tiles x * per_xcd, x * per_xcd + 1, ...
+    const int lid = (blockIdx.x & 7) * fg.per_xcd + (blockIdx.x >> 3);
+    if (lid >= fg.total) return;
+    const int chunk = lid % fg.chunks, tile = lid / fg.chunks;
+    const int strip = tile % fg.strips, band = tile / fg.strips;
+    const int x0 = strip * XB, d0 = chunk * DC;
+    const int y0 = band * fg.band_rows, y1 = min(fg.ncomp, y0 + fg.band_rows);
+    const int nv = (y1 - y0) + 2 * SH2;                      // rows of P the band needs
+    const int t = threadIdx.x;
+    uint32_t* S0 = lds_fuse;                                 // staging, two buffers
+    uint32_t* V0 = lds_fuse + 2 * fz.stage_words();          // V rows [NX][DPC], two buffers
+    const int xs = g.minX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
+    const int xr0 = xs - g.minD - (d0 + DC - 1);             // right entry r <-> xr0 + r
+    const size_t plane = (size_t)g.W * g.H;
+    auto stage = [&](int v, uint32_t* S) {                   // row of virtual row v, by waves 4-7
+        const int st = t - 256;
+        const int k_img = min(max(y0 - SH2 + v, 0), g.H - 1);
+        uint32_t* Lx = S;
+        uint16_t* Rh = (uint16_t*)(S + 6 * NX);
+        for (int i = st; i < 2 * NX; i += 256) {
+            const int c = i >= NX, k = i - c * NX;
+            const uint32_t w = bt[c * plane + (size_t)k_img * g.W + min(max(xs + k, 0), g.W - 1)];
+            uint32_t* o = Lx + 6 * k + 3 * c;
+            o[0] = (w & 0xFFu) * 0x10001u; o[1] = ((w >> 8) & 0xFFu) * 0x10001u; o[2] = ((w >> 16) & 0xFFu) * 0x10001u;
+        }
+        const int NRr = NX + DC - 1;
+        for (int i = st; i < 2 * NRr; i += 256) {
+            const int c = i >= NRr, r = i - c * NRr;
+            const uint32_t w = bt[(2 + c) * plane + (size_t)k_img * g.W + min(max(xr0 + r, 0), g.W - 1)];
+            const int j = M - 1 - r;
+            uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
+            uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
+            const uint16_t v = w & 0xFF, lo = (w >> 8) & 0xFF, hi = (w >> 16) & 0xFF;
+            lo16[0] = v; lo16[2] = lo; lo16[4] = hi;
+            hi16[0] = v; hi16[2] = lo; hi16[4] = hi;
+        }
+    };
+    // P + ring + V: staged column kc, pairs tq*I .. tq*I + I - 1
+    const int kc = t / TPC, tq = t % TPC;
+    uint32_t ring[I][R];
+    uint32_t Vs[I];
+#pragma unroll
+    for (int q = 0; q < I; q++) {
+        Vs[q] = 0;
+#pragma unroll
+        for (int s = 0; s < R; s++) ring[q][s] = 0;
+    }
+    auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
+    auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
+    // box: thread (segment, pair) of waves 0-3
+    const int nout = min(XB, g.width1 - x0);
+    const int klo = max(SW2 - x0, 0), khi = min(g.width1 - 1 - x0 + SW2, NX - 1);
+    constexpr int NSEG = 256 / DPC;
+    const int bp = t % DPC, bseg = t / DPC;
+    const int seglen = (nout + NSEG - 1) / NSEG;
+    const int xa = bseg * seglen, xb = min(xa + seglen, nout);
+    u16x2_t bmax = {0, 0};                                   // flag: the largest box sum seen
+    const bool col0 = (g.compat & SGM_OCV_COL0_LEGACY) && x0 == 0;
+    const u16x2_t p2v = {(unsigned short)g.P2, (unsigned short)g.P2};
+    uint32_t* C32 = (uint32_t*)C;
+    const size_t rowC = (size_t)g.width1 * g.D / 2;         // u32 per C' row
+    auto box = [&](int y, const uint32_t* V, bool tail) {   // output row y (waves 0-3)
+        if (xa >= xb) return;
+        const uint32_t* Vp = V + bp;
+        auto rd = [&](int k) { return __builtin_bit_cast(u16x2_t, Vp[min(max(k, klo), khi) * DPC]); };
+        u16x2_t sum = {0, 0};
+        for (int u = 0; u <= 2 * SW2; u++) sum += rd(xa + u);
+        uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * g.D + d0) / 2 + bp;
+        for (int xo = xa; xo < xb; xo++) {
+            if (xo > xa) sum += rd(xo + 2 * SW2) - rd(xo - 1);
+            if (!(col0 && xo == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
+            const uint32_t c = __builtin_bit_cast(uint32_t, sum + p2v);
+            o[0] = c;
+            if (tail)                                        // OpenCV's bottom rows: never recomputed
+                for (int yy = y + 1; yy < g.H; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? g.P2 * 0x10001u : c;
+            o += g.D / 2;
+        }
+    };
+    if (t >= 256) stage(0, S0);
+    __syncthreads();
+    const bool last_band = y1 == fg.ncomp;
+    for (int vb = 0; vb <= nv; vb += R) {
+        static_for<0, R>([&](auto jj) {
+            constexpr int s = decltype(jj)::value;
+            const int v = vb + s;
+            if (v > nv) return;                              // uniform
+            uint32_t* S = S0 + (v & 1) * fz.stage_words();
+            if (v < nv) {
+                const uint32_t* Lk = S + 6 * kc;
+                u16x2_t u[2], ulo[2], uhi[2];
+#pragma unroll
+                for (int c = 0; c < 2; c++) { u[c] = wd(Lk, 3 * c); ulo[c] = wd(Lk, 3 * c + 1); uhi[c] = wd(Lk, 3 * c + 2); }
+                const int j0 = M - DC - kc + 2 * tq * I;
+                const uint32_t* Rk = S + 6 * NX + 7 * ((j0 & 1) * MH + (j0 >> 1));
+                uint32_t* Vout = V0 + (v & 1) * NX * DPC + kc * DPC + tq * I;
+#pragma unroll
+                for (int q = 0; q < I; q++) {
+                    u16x2_t m[2];
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const u16x2_t vv = wd(Rk, 7 * q + 3 * c), v0 = wd(Rk, 7 * q + 3 * c + 1), v1 = wd(Rk, 7 * q + 3 * c + 2);
+                        const u16x2_t c0 = __builtin_elementwise_max(sat(u[c], v1), sat(v0, u[c]));
+                        const u16x2_t c1 = __builtin_elementwise_max(sat(vv, uhi[c]), sat(ulo[c], vv));
+                        m[c] = __builtin_elementwise_min(c0, c1);
+                    }
+                    const uint32_t P = __builtin_bit_cast(uint32_t, m[0] + (m[1] >> (u16x2_t){2, 2}));
+                    Vs[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, Vs[q]) + __builtin_bit_cast(u16x2_t, P) -
+                                                         __builtin_bit_cast(u16x2_t, ring[q][s]));
+                    ring[q][s] = P;
+                }
+                if (v >= 2 * SH2) {
+                    if constexpr (I == 4) {
+                        *(uint4*)Vout = make_uint4(Vs[0], Vs[1], Vs[2], Vs[3]);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
+                    }
+                }
+            }
+            if (t < 256) {
+                if (v >= 1 && v - 1 >= 2 * SH2) {
+                    const int y = y0 + (v - 1) - 2 * SH2;
+                    box(y, V0 + ((v - 1) & 1) * NX * DPC, last_band && y == fg.ncomp - 1);
+                }
+            } else if (v + 1 < nv) {
+                stage(v + 1, S0 + ((v + 1) & 1) * fz.stage_words());
+            }
+            __syncthreads();
+        });
+    }
+    if (g.wide == 2 && g.ovf && t < 256) {
+        const int m = max((int)bmax[0], (int)bmax[1]);
+        const bool ovf = m > g.ovf_thr - g.P2;
+        const uint64_t b = __ballot(ovf);
+        if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(g.ovf, 1);
+    }
+}
+
+// COL0_LEGACY after the fused cost: column x1 = 0 of rows y >= 1 holds row 0's value (MODE_SGBM's
+// single C row is never updated there) or the P2 initialisation (MODE_HH)
+__global__ __launch_bounds__(256) void k_ocv_col0_legacy(Geom g, int fullDP, int16_t* __restrict__ C)
+{
+    const int d = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y + 1;
+    if (d >= g.D) return;
+    C[(size_t)y * g.width1 * g.D + d] = fullDP ? (int16_t)g.P2 : C[d];
+}
+
+// The fused cost applies: R = 2*SH2 + 1 <= 21 (the register ring; SH2 <= 10 leaves XB >= 108 of
+// the 128 staged columns) and every sum exact in u16.
+__host__ inline bool ocv_cost_fusable(const Geom& g)
+{
+    const long long B = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63);
+    const char* e = std::getenv("SGM_OCV_FUSED");
+    return g.SH2 <= 10 && g.SW2 <= 10 && B <= 65535 && g.width1 > 0 && e && std::atoi(e) != 0;
+}
+
+// The SIMD_SAT flagged frames whose horizontal sums cannot saturate: when
+// (2*SW2 + 1) * (2*ftzero + 63) <= 32767 every running horizontal sum of the SIMD loop stays in
+// int16 (it is a box of pixel costs <= 2*ftzero + 63, and (h - sub) + add never leaves
+// [-maxP, 32767]), so the plain horizontal sums hs (k_ocv_pixhsum) ARE the SIMD branch's and only
+// the vertical update saturates: C_y = sat(sat(C_{y-1} - hs[y-SH2-1]) + hs[y+SH2]). That chain is
+// sequential per (column, d), so a thread owns a pair of adjacent disparities (packed saturating
+// i16 ops, v_pk_sub_i16 / v_pk_add_i16 with clamp) and walks every row; the grid covers
+// width1 * D / 2 pairs (437 K threads at the shipped 2448x2048 D=480 config). Each hs row is read
+// from HBM once, as it enters the window, U rows ahead of the chain, and kept in the thread's
+// LDS ring (R = 2*SH2 + 1 slots) until it leaves: 2 B read + 2 B written per cell. The old
+// k_ocv_pixcost_sat / k_ocv_hsum_sat / k_ocv_vsum_sat chain (one int16 per thread, no prefetch)
+// stays for the configs whose horizontal sums can saturate (boxes wider than ~171 columns).
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__host__ __device__ inline bool ocv_hsum_cannot_saturate(const Geom& g)
+{
+    return (2 * g.SW2 + 1) * (2 * g.ftzero + 63) <= 32767;
+}
+__host__ inline int vsum_sat2_unroll(const Geom& g)
+{
+    const int R = 2 * g.SH2 + 1;
+    return R >= 8 ? 8 : R >= 4 ? 4 : R >= 2 ? 2 : 1;
+}
+template <int U>
+__global__ __launch_bounds__(256) void k_ocv_vsum_sat2(const int16_t* __restrict__ hs, Geom g, int fullDP,
+                                                       int16_t* __restrict__ C)
+{
+    if (!ocv_flagged(g)) return;
+    extern __shared__ uint32_t ring_sat[];                 // [R][256]: slot s of thread t at s * 256 + t
+    const int t = threadIdx.x, i = blockIdx.x * 256 + t;
+    const size_t rs = (size_t)g.width1 * g.D / 2;           // u32 pairs per row
+    if (i >= (int)rs) return;                               // no barriers below: the ring is per thread
+    const uint32_t* h32 = (const uint32_t*)hs;
+    uint32_t* C32 = (uint32_t*)C;
+    const int H = g.H, SH2 = g.SH2, R = 2 * SH2 + 1;
+    uint32_t* ring = ring_sat + t;
+    auto lo16 = [](uint32_t w) { return (int)(int16_t)(uint16_t)w; };
+    auto hi16 = [](uint32_t w) { return (int)w >> 16; };
+    auto S = [](uint32_t w) { return __builtin_bit_cast(s16x2_t, w); };
+    // row 0: P2 + the clamped window, int sums wrapped to int16 (the scalar y == 0 loop)
+    int s0 = 0, s1 = 0;
+    for (int k = 0; k <= SH2; k++) {
+        const uint32_t w = h32[(size_t)min(k, H - 1) * rs + i];
+        if (k < H) ring[k * 256] = w;                       // rows 0 .. SH2 enter the ring (k < R)
+        const int m = k == 0 ? SH2 + 1 : 1;                 // row 0 weighs SH2 + 1 (clamped rows above)
+        s0 += m * lo16(w); s1 += m * hi16(w);
+    }
+    uint32_t c = ((uint32_t)(g.P2 + s0) & 0xFFFFu) | ((uint32_t)(g.P2 + s1) << 16);
+    C32[i] = c;
+    const bool col0 = (g.compat & SGM_OCV_COL0_LEGACY) && i < g.D / 2;
+    const uint32_t p2w = ((uint32_t)g.P2 & 0xFFFFu) * 0x10001u;
+    const int ylast = H - SH2 - 1;                           // rows y <= ylast add row y + SH2
+    // ring slot of row y - SH2 - 1 (= the slot row y + SH2 takes: they are R rows apart), kept
+    // as a running counter (no modulo in the loop); rows y <= SH2 subtract row 0 (slot 0) and
+    // add row y + SH2 < R into slot y + SH2
+    int q0 = (R - SH2) % R;                                  // its value at y = 1
+    for (int yb = 1; yb < H; yb += U) {
+        uint32_t add[U], sub[U];
+        int slot[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {                        // entering rows (clamped: used only if y <= ylast)
+            const int y = yb + u;
+            int q = q0 + u;
+            q = q >= R ? q - R : q;                          // U <= R
+            slot[u] = y <= SH2 ? y + SH2 : q;
+            add[u] = h32[(size_t)min(y + SH2, H - 1) * rs + i];
+            sub[u] = ring[(y <= SH2 ? 0 : q) * 256];         // leaving rows: none of this group's (U <= R)
+        }
+        q0 += U;
+        q0 = q0 >= R ? q0 - R : q0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int y = yb + u;
+            if (y >= H) break;
+            if (y <= ylast) {
+                if (!col0)
+                    c = __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(
+                            __builtin_elementwise_sub_sat(S(c), S(sub[u])), S(add[u])));
+                else if (fullDP)
+                    c = p2w;
+                ring[slot[u] * 256] = add[u];
+            } else if (fullDP) {
+                c = p2w;                                     // MODE_HH: never recomputed, the P2 init
+            }                                                // MODE_SGBM: the last computed row
+            C32[(size_t)y * rs + i] = c;
+        }
     }
 }
 
@@ -1099,30 +1410,115 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
 // ------------------------------------------------------------------------------------
 static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <= 128 ? 8 : D <= 256 ? 16 : 32; }
 
-// C' of the frame into bufA. SIMD_SAT frames that take the flagged kernels (Geom::wide != 0 and
-// the overflow flag) get the exact SIMD cost, sequential, into bufB (pixel costs -> bufB,
-// horizontal sums -> bufA, C' -> bufB): ocv_cost_buffer() says which one the paths read.
+// C' of the frame into bufA (bufB: scratch, the horizontal sums). SIMD_SAT frames that take
+// the flagged kernels (Geom::wide != 0 and the overflow flag) get the exact SIMD cost written
+// over it, by kernels that return at once on the other frames: the vertical SIMD update over
+// the plain horizontal sums (k_ocv_vsum_sat2) when those cannot saturate, else the sequential
+// chain (pixel costs -> bufA, horizontal sums -> bufB, C' -> bufA).
+template <int R>
+static void launch_cost_fused_r(const uint32_t* bt, const Geom& g, int fullDP, const FuseGrid& fg, int16_t* C,
+                                hipStream_t st)
+{
+    const dim3 grid(fg.per_xcd * 8), block(kFuseThreads);
+    if constexpr (R <= 9) {
+        if (g.D % 64 == 0) {
+            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8>), grid, block, FuseGeo(32).lds_bytes(32), st, bt, g, fullDP, fg, C);
+            return;
+        }
+    }
+    if (g.D % 32 == 0)
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4>), grid, block, FuseGeo(16).lds_bytes(16), st, bt, g, fullDP, fg, C);
+    else
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2>), grid, block, FuseGeo(8).lds_bytes(8), st, bt, g, fullDP, fg, C);
+}
+
+static FuseGrid fuse_grid(const Geom& g)
+{
+    FuseGrid fg{};
+    const int dpc = (2 * g.SH2 + 1 <= 9 && g.D % 64 == 0) ? 32 : g.D % 32 == 0 ? 16 : 8;
+    const int XB = fuse_xb(g);
+    fg.strips = (g.width1 + XB - 1) / XB;
+    fg.chunks = g.D / (2 * dpc);
+    fg.ncomp = std::max(g.H - g.SH2 - 1, 0) + 1;             // rows 0 .. ylast are computed
+    const long long tiles = (long long)fg.strips * fg.chunks;
+    const char* e = std::getenv("SGM_FUSE_ROWS");
+    fg.band_rows = e ? std::max(std::atoi(e), 1)
+                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
+    fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
+    fg.total = (int)(tiles * fg.bands);
+    fg.per_xcd = (fg.total + 7) / 8;
+    return fg;
+}
+
+// C' of the frame into bufA (bufB: scratch, the horizontal sums of the unfused kernels).
+// Default: k_ocv_btplanes + k_ocv_cost_fused (+ k_ocv_col0_legacy) when ocv_cost_fusable, else
+// k_ocv_pixhsum (or k_ocv_pixcost + k_ocv_hsum) + k_ocv_vsum_seg. SIMD_SAT frames that take the
+// flagged kernels (Geom::wide != 0 and the overflow flag) get the exact SIMD cost written over
+// it, by kernels that return at once on the other frames: the vertical SIMD update over the
+// plain horizontal sums (k_ocv_vsum_sat2; after the fused cost, a gated k_ocv_pixhsum makes
+// those sums first) when the horizontal sums cannot saturate, else the sequential chain
+// (pixel costs -> bufA, horizontal sums -> bufB, C' -> bufA).
 hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, const Geom& g, int fullDP,
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
 {
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes);
     const size_t lds = pix_lds_bytes(g);
-    if (lds <= 64 * 1024) {
-        const int XB = pix_xb(g), DC = pix_dc(g);
-        hipLaunchKernelGGL(k_ocv_pixhsum, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256), lds, st,
-                           planes, g, bufB);
-    } else {                // very wide boxes x wide ranges: the unfused pair (no LDS staging)
-        hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
-        hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
+    const bool fused = ocv_cost_fusable(g);
+    const bool sat2 = g.wide && (g.compat & SGM_OCV_SIMD_SAT) && ocv_hsum_cannot_saturate(g) &&
+                      (size_t)(2 * g.SH2 + 1) * 256 * 4 <= 64 * 1024 && !std::getenv("SGM_OCV_SAT_SEQ");
+    if (fused) {
+        uint32_t* bt = (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H));
+        hipLaunchKernelGGL(k_ocv_btplanes, dim3((g.W + 255) / 256, g.H, 4), dim3(256), 0, st, planes, g.W, g.H, bt);
+        const FuseGrid fg = fuse_grid(g);
+        switch (g.SH2) {
+        case 0: launch_cost_fused_r<1>(bt, g, fullDP, fg, bufA, st); break;
+        case 1: launch_cost_fused_r<3>(bt, g, fullDP, fg, bufA, st); break;
+        case 2: launch_cost_fused_r<5>(bt, g, fullDP, fg, bufA, st); break;
+        case 3: launch_cost_fused_r<7>(bt, g, fullDP, fg, bufA, st); break;
+        case 4: launch_cost_fused_r<9>(bt, g, fullDP, fg, bufA, st); break;
+        case 5: launch_cost_fused_r<11>(bt, g, fullDP, fg, bufA, st); break;
+        case 6: launch_cost_fused_r<13>(bt, g, fullDP, fg, bufA, st); break;
+        case 7: launch_cost_fused_r<15>(bt, g, fullDP, fg, bufA, st); break;
+        case 8: launch_cost_fused_r<17>(bt, g, fullDP, fg, bufA, st); break;
+        case 9: launch_cost_fused_r<19>(bt, g, fullDP, fg, bufA, st); break;
+        default: launch_cost_fused_r<21>(bt, g, fullDP, fg, bufA, st); break;
+        }
+        if ((g.compat & SGM_OCV_COL0_LEGACY) && g.H > 1)
+            hipLaunchKernelGGL(k_ocv_col0_legacy, dim3((g.D + 255) / 256, g.H - 1), dim3(256), 0, st, g, fullDP, bufA);
+        if (sat2) {                    // the flagged frames' horizontal sums for k_ocv_vsum_sat2
+            const int XB = pix_xb(g), DC = pix_dc(g);
+            hipLaunchKernelGGL(k_ocv_pixhsum<true>, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256),
+                               lds, st, planes, g, bufB);
+        }
+    } else {
+        if (lds <= 64 * 1024) {
+            const int XB = pix_xb(g), DC = pix_dc(g);
+            hipLaunchKernelGGL(k_ocv_pixhsum<false>, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256),
+                               lds, st, planes, g, bufB);
+        } else {            // very wide boxes x wide ranges: the unfused pair (no LDS staging)
+            hipLaunchKernelGGL(k_ocv_pixcost, dim3(g.width1, g.H), dim3(256), 0, st, planes, g, bufA);
+            hipLaunchKernelGGL(k_ocv_hsum, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
+        }
+        hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D / 2 + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows),
+                           dim3(256), 0, st, bufB, g, fullDP, bufA);
     }
-    hipLaunchKernelGGL(k_ocv_vsum_seg, dim3((g.width1 * g.D / 2 + 255) / 256, (g.H + kVsumRows - 1) / kVsumRows), dim3(256),
-                       0, st, bufB, g, fullDP, bufA);
     if (g.wide && (g.compat & SGM_OCV_SIMD_SAT)) {
         const size_t rc = (size_t)g.width1 * g.D;
-        hipLaunchKernelGGL(k_ocv_pixcost_sat, dim3(std::min(g.width1 * g.H, 8192)), dim3(256), 0, st, planes, g, bufB);
-        hipLaunchKernelGGL(k_ocv_hsum_sat, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufB, g, bufA);
-        hipLaunchKernelGGL(k_ocv_vsum_sat, dim3((unsigned)((rc + 255) / 256)), dim3(256), 0, st, bufA, g, fullDP, bufB);
+        if (sat2) {
+            const size_t ring = (size_t)(2 * g.SH2 + 1) * 256 * 4;
+            const dim3 grid((unsigned)((rc / 2 + 255) / 256));
+            switch (vsum_sat2_unroll(g)) {
+            case 8: hipLaunchKernelGGL(k_ocv_vsum_sat2<8>, grid, dim3(256), ring, st, bufB, g, fullDP, bufA); break;
+            case 4: hipLaunchKernelGGL(k_ocv_vsum_sat2<4>, grid, dim3(256), ring, st, bufB, g, fullDP, bufA); break;
+            case 2: hipLaunchKernelGGL(k_ocv_vsum_sat2<2>, grid, dim3(256), ring, st, bufB, g, fullDP, bufA); break;
+            default: hipLaunchKernelGGL(k_ocv_vsum_sat2<1>, grid, dim3(256), ring, st, bufB, g, fullDP, bufA); break;
+            }
+        } else {
+            hipLaunchKernelGGL(k_ocv_pixcost_sat, dim3(std::min(g.width1 * g.H, 8192)), dim3(256), 0, st, planes, g, bufA);
+            hipLaunchKernelGGL(k_ocv_hsum_sat, dim3((g.D + 255) / 256, g.H), dim3(256), 0, st, bufA, g, bufB);
+            hipLaunchKernelGGL(k_ocv_vsum_sat, dim3((unsigned)((rc + 255) / 256)), dim3(256), 0, st, bufB, g, fullDP, bufA);
+        }
     }
     return hipGetLastError();
 }

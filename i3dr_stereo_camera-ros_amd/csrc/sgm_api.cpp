@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -363,7 +364,7 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
             }
         }
     } else {
-        l.planes = take(WH * 4);
+        l.planes = take(sgm::ocv_planes_total(g.W, g.H));
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
         const size_t es = g.wide && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // int32 / int16 path volumes
@@ -471,9 +472,17 @@ bool ocv_vwta_on(const Geom& g, int fullDP)
     return (double)g.width1 * g.H * g.D >= (fullDP ? 2.0e8 : 1.0e9);
 }
 
+// Rows of the output that are final, in order, while the pipeline is still running: the census
+// WTA in `chunks` row bands (no post filter follows it), `done(y0, y1)` called after each band's
+// launch is queued on h->stream (match_host's chunked copy-out).
+struct RowsHook {
+    int chunks = 1;
+    std::function<int(int, int)> done;
+};
+
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
-                 int16_t* dOut, size_t out_stride)
+                 int16_t* dOut, size_t out_stride, const RowsHook* hook = nullptr)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
@@ -506,7 +515,23 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
-        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
+        if (hook && hook->chunks > 1 && !med && p.speckle_window_size <= 0) {
+            // one WTA launch per row band (a row's WTA, disp2 and LR need only its own row)
+            const size_t vrow = (size_t)g.width1 * g.D;
+            for (int c = 0; c < hook->chunks; c++) {
+                const int y0 = (int)((long long)c * g.H / hook->chunks), y1 = (int)((long long)(c + 1) * g.H / hook->chunks);
+                if (y1 <= y0) continue;
+                Geom gc = g;
+                gc.H = y1 - y0;
+                sgm::WtaFrames wc = wf;
+                wc.vols[0] = vols + (size_t)y0 * vrow;
+                wc.out[0] = dst + (size_t)y0 * dst_stride;
+                HIP_TRY(sgm::launch_census_wta(wc, l.vol_bytes, gc, dst_stride, st), "wta");
+                if (int r = hook->done(y0, y1)) return r;
+            }
+        } else {
+            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
+        }
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -530,16 +555,16 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
             uint64_t* res = (uint64_t*)(ws + l.ores);
             // the unfused stages' byte basis (C' counted once, in the paths stage)
             rec.begin("ocv_paths", 2 * cells + es * cells * (ndir - 1));
-            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st, fd), "ocv_paths");
+            HIP_TRY(sgm::launch_ocv_paths(A, A, V, ncells, gg, mask, st, fd), "ocv_paths");
             rec.begin("ocv_vwta", es * cells * (ndir - 1) + 8 * WH);
-            HIP_TRY(sgm::launch_ocv_vwta(A, B, V, ncells, ndir, gg, res, st), "ocv_vwta");
+            HIP_TRY(sgm::launch_ocv_vwta(A, A, V, ncells, ndir, gg, res, st), "ocv_vwta");
             sgm::WtaFrames wf{};
             wf.res[0] = res; wf.out[0] = dst; wf.n = 1;
             rec.begin("ocv_rowfin", 8 * WH + 2 * WH);
             HIP_TRY(sgm::launch_census_rowfin(wf, g, dst_stride, st), "ocv_rowfin");
         } else {
             rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
-            HIP_TRY(sgm::launch_ocv_paths(A, B, V, ncells, gg, mask, st), "ocv_paths");
+            HIP_TRY(sgm::launch_ocv_paths(A, A, V, ncells, gg, mask, st), "ocv_paths");
             rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
             HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
         }
@@ -816,6 +841,32 @@ int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H,
 // profiles/r03_host_copy.txt), a pageable 1920x1080 H2D takes 58 us against 42 us of CPU
 // packing + 45 us of pinned DMA, and the 8.3 MB float D2H runs at the same 53 GB/s into
 // pageable or pinned memory — staging buffers would only add copies.
+// Is [p, p + bytes) page-locked host memory (sgm_host_register / hipHostMalloc)?
+bool host_pinned(const void* p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Rows per copy-out chunk of a pinned host output (census frames without post filters): the
+// WTA runs in kOutChunks row bands and band i's rows go back on the `down` stream while band
+// i + 1 is matched, so only the last band's copy adds to the call.
+constexpr int kOutChunks = 4;
+
+int ensure_down(sgm_handle* h)
+{
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    if (!h->down) HIP_TRY(hipStreamCreateWithPriority(&h->down, hipStreamNonBlocking, hi), "hipStreamCreate");
+    while (h->io_ev.size() < (size_t)kOutChunks) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        h->io_ev.push_back(e);
+    }
+    return SGM_OK;
+}
+
 int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, void* out,
                size_t out_stride, bool f32)
 {
@@ -829,14 +880,38 @@ int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, 
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, st), "H2D L");
     HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
     int16_t* d16 = (int16_t*)(ws + l.out);
-    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
-    if (rc) return rc;
-    const void* dsrc = d16;
-    if (f32) {
-        HIP_TRY(sgm::launch_to_f32(d16, W, (float*)(ws + l.outf), W, W, H, st), "to_f32");
-        dsrc = ws + l.outf;
+    float* df = (float*)(ws + l.outf);
+    const void* dsrc = f32 ? (const void*)df : (const void*)d16;
+    // copy rows [y0, y1) out (y0 < 0: the whole frame) on stream `cs`
+    auto copy_out = [&](int y0, int y1, hipStream_t cs, int chunk) -> int {
+        if (y0 < 0) { y0 = 0; y1 = H; }
+        if (f32) HIP_TRY(sgm::launch_to_f32(d16 + (size_t)y0 * W, W, df + (size_t)y0 * W, W, W, y1 - y0, st), "to_f32");
+        if (cs != st) {
+            hipEvent_t ev = h->io_ev[chunk % kOutChunks];
+            HIP_TRY(hipEventRecord(ev, st), "hipEventRecord");
+            HIP_TRY(hipStreamWaitEvent(cs, ev, 0), "hipStreamWaitEvent");
+        }
+        HIP_TRY(hipMemcpy2DAsync((char*)out + (size_t)y0 * out_stride * es, out_stride * es,
+                                 (const char*)dsrc + (size_t)y0 * W * es, W * es, W * es, y1 - y0,
+                                 hipMemcpyDeviceToHost, cs), "D2H");
+        return SGM_OK;
+    };
+    const bool chunked = h->params.mode == SGM_MODE_CENSUS8 && !use_median(h->params) &&
+                         h->params.speckle_window_size <= 0 && g.width1 > 0 && H >= 2 * kOutChunks && host_pinned(out);
+    if (chunked) {
+        if ((rc = ensure_down(h))) return rc;
+        RowsHook hook;
+        hook.chunks = kOutChunks;
+        int chunk = 0;
+        hook.done = [&](int y0, int y1) { return copy_out(y0, y1, h->down, chunk++); };
+        rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W, &hook);
+        if (rc) { (void)hipStreamSynchronize(st); (void)hipStreamSynchronize(h->down); return rc; }
+        HIP_TRY(hipStreamSynchronize(h->down), "sync down");
+    } else {
+        rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
+        if (rc) return rc;
+        if ((rc = copy_out(-1, -1, st, 0))) return rc;
     }
-    HIP_TRY(hipMemcpy2DAsync(out, out_stride * es, dsrc, W * es, W * es, H, hipMemcpyDeviceToHost, st), "D2H");
     HIP_TRY(hipStreamSynchronize(st), "sync");
     return mark_done(h, st);
 }
@@ -930,6 +1005,24 @@ int sgm_get_params(const sgm_handle* h, sgm_params* p)
 }
 
 int sgm_abi_version(void) { return SGM_ABI_VERSION; }
+
+int sgm_host_register(sgm_handle* h, void* ptr, size_t bytes)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!ptr || !bytes) return fail(h, SGM_ERR_ARG, "null or empty host range");
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
+    return SGM_OK;
+}
+
+int sgm_host_unregister(sgm_handle* h, void* ptr)
+{
+    if (!h) return SGM_ERR_ARG;
+    if (!ptr) return fail(h, SGM_ERR_ARG, "null host pointer");
+    HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
+    return SGM_OK;
+}
 
 int sgm_check_params(const sgm_params* p, int width, int height)
 {
@@ -2092,10 +2185,11 @@ int sgm_debug_ocv_cost(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W,
             "ocv_cost");
     if (g.wide == 2) HIP_TRY(hipMemcpyAsync(&flag, g.ovf, sizeof(int), hipMemcpyDeviceToHost, h->stream), "D2H flag");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
-    // SIMD_SAT frames in the overflow regime: the sequential saturating cost (bufB)
-    const bool simd = (g.wide == 1 || (g.wide == 2 && flag)) && (g.compat & SGM_OCV_SIMD_SAT);
+    // C' of every frame kind ends in bufA (SIMD_SAT frames in the overflow regime: the exact
+    // saturating cost, written over the plain one)
+    (void)flag;
     const size_t cells = (size_t)g.width1 * g.H * g.D;
-    HIP_TRY(hipMemcpyAsync(cost, simd ? B : A, cells * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
+    HIP_TRY(hipMemcpyAsync(cost, A, cells * 2, hipMemcpyDeviceToHost, h->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(h->stream), "sync");
     return SGM_OK;
 }

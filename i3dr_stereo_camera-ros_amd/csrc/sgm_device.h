@@ -51,6 +51,11 @@ struct Geom {
                             // 32767 - P2 under SIMD_SAT: (short)(minLr + P2) must not wrap)
 };
 
+// OCV workspace: the four u8 prefilter planes, then (256-B aligned) the four u32 planes of
+// packed Birchfield-Tomasi intervals that the fused cost stages per row.
+__host__ __device__ inline size_t ocv_planes_bytes(int W, int H) { return ((size_t)W * H * 4 + 255) / 256 * 256; }
+__host__ __device__ inline size_t ocv_planes_total(int W, int H) { return ocv_planes_bytes(W, H) + (size_t)W * H * 16; }
+
 // Elements of one OCV path volume of `cells` cells at es bytes per cell (256-B aligned
 // slices; the host layout and the kernels' launchers agree on it).
 __host__ __device__ inline size_t ocv_vol_elems(size_t cells, size_t es) { return (cells * es + 255) / 256 * 256 / es; }

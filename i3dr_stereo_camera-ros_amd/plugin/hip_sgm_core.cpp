@@ -53,7 +53,24 @@ MatcherCore::MatcherCore(int device, int mode) : device_(device)
     params_.prefilter_cap = params_.speckle_window_size = params_.speckle_range = 0;
 }
 
-MatcherCore::~MatcherCore() { sgm_destroy(handle_); }
+MatcherCore::~MatcherCore()
+{
+    releaseOutput();
+    sgm_destroy(handle_);
+}
+
+void MatcherCore::keepOutputRegistered(bool enable)
+{
+    keep_reg_ = enable;
+    if (!enable) releaseOutput();
+}
+
+void MatcherCore::releaseOutput()
+{
+    if (reg_ptr_ && handle_) (void)sgm_host_unregister(handle_, reg_ptr_);
+    reg_ptr_ = nullptr;
+    reg_bytes_ = 0;
+}
 
 void MatcherCore::setDisparityRange(int r, int image_width)
 {
@@ -91,6 +108,14 @@ int MatcherCore::run(const sgm_params& p, const uint8_t* a, const uint8_t* b, in
     int rc = SGM_OK;
     if (!handle_) rc = sgm_create(&handle_, device_);
     if (rc == SGM_OK) rc = sgm_set_params(handle_, &p);
+    if (rc == SGM_OK && keep_reg_ && outf) {
+        const size_t bytes = out_stride * sizeof(float) * (size_t)(h - 1) + (size_t)w * sizeof(float);
+        if (reg_ptr_ != (void*)outf || reg_bytes_ != bytes) {
+            releaseOutput();
+            // not fatal: an unregistered output takes one synchronous copy
+            if (sgm_host_register(handle_, outf, bytes) == SGM_OK) { reg_ptr_ = outf; reg_bytes_ = bytes; }
+        }
+    }
     if (rc == SGM_OK)
         rc = outf ? sgm_match_f32(handle_, a, b, w, h, stride, outf, out_stride)
                   : sgm_match(handle_, a, b, w, h, stride, out16, out_stride);

@@ -56,6 +56,12 @@ public:
     int backwardMatch16(const uint8_t* left, const uint8_t* right, int width, int height, size_t stride,
                         int16_t* out, size_t out_stride);
 
+    // Keep the forwardMatch output buffer page-locked between frames (sgm_host_register) so the
+    // copy-out overlaps the match; the caller must call releaseOutput() before that buffer is
+    // freed or reallocated (MatcherHIPSGM: before disparity_lr.create() changes its size/type).
+    void keepOutputRegistered(bool enable);
+    void releaseOutput();
+
     const sgm_params& params() const { return params_; }
     bool interpolation() const { return interpolate_; }
     int disparityRange() const { return params_.num_disparities; }
@@ -69,6 +75,9 @@ private:
     sgm_handle* handle_ = nullptr;   // opened lazily at the first match
     sgm_params params_{};
     bool interpolate_ = false;
+    bool keep_reg_ = false;
+    void* reg_ptr_ = nullptr;        // the registered output range
+    size_t reg_bytes_ = 0;
     std::string err_;
 };
 

@@ -7,6 +7,8 @@ void MatcherHIPSGM::init(void)
   // Setup for 16-bit disparity, like MatcherOpenCVSGBM::init (device opened lazily)
   cv::Mat(image_size, CV_16S).copyTo(disparity_lr);
   cv::Mat(image_size, CV_16S).copyTo(disparity_rl);
+  // disparity_lr persists across frames: keep it page-locked (released before it is reallocated)
+  core_.keepOutputRegistered(true);
 }
 
 int MatcherHIPSGM::forwardMatch()
@@ -22,10 +24,16 @@ int MatcherHIPSGM::forwardMatch()
     // disparity (CV_16S in disparity_rl) replaces disparity_lr
     int rc = backwardMatch();
     if (rc == 0)
+    {
+      if (disparity_lr.size() != disparity_rl.size() || disparity_lr.type() != CV_32FC1)
+        core_.releaseOutput();  // convertTo reallocates disparity_lr
       disparity_rl.convertTo(disparity_lr, CV_32FC1);
+    }
     return rc;
   }
   // CV_32FC1 straight from the device (matcherOpenCVSGBM.cpp:34's convertTo runs there)
+  if (disparity_lr.size() != left->size() || disparity_lr.type() != CV_32FC1)
+    core_.releaseOutput();  // create() reallocates: unregister the old buffer before it is freed
   disparity_lr.create(left->size(), CV_32FC1);
   return core_.forwardMatch(left->data, right->data, left->cols, left->rows, left->step,
                             (float *)disparity_lr.data, disparity_lr.step / sizeof(float));

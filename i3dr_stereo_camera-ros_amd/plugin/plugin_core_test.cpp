@@ -94,6 +94,9 @@ int main(int argc, char** argv)
         m.setPreFilterCap(31);
         m.setP1(200);
         m.setP2(400);
+        if (argc > 11) m.setSpeckleFilterWindow(std::atoi(argv[11]));
+        // the adapter keeps its persistent disparity_lr page-locked (matcherHIPSGM.cpp init)
+        m.keepOutputRegistered(argc > 12 ? std::atoi(argv[12]) != 0 : true);
         std::vector<float> d((size_t)W * H);
         if (m.forwardMatch(L.data(), R.data(), W, H, W, d.data(), W) != 0) return fail("match");   // warm-up
         std::vector<double> t;

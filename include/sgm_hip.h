@@ -109,6 +109,15 @@ int  sgm_device_count(void);
 int  sgm_create(sgm_handle** out, int device);
 void sgm_destroy(sgm_handle* h);
 
+/* Page-lock a caller's host buffer (hipHostRegister) for as long as it stays registered. A
+ * registered output of sgm_match / sgm_match_f32 is filled by asynchronous copies that overlap
+ * the end of the match (census frames without post filters: the WTA runs in row bands and each
+ * band's rows go back while the next is matched); unregistered memory takes one synchronous copy
+ * after the match. The caller must unregister a buffer before freeing it (the MatcherHIPSGM
+ * adapter registers its persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat).      */
+int  sgm_host_register(sgm_handle* h, void* ptr, size_t bytes);
+int  sgm_host_unregister(sgm_handle* h, void* ptr);
+
 /* Defaults: census mode = north-star config (P1 10, P2 120, uniq 5, subpixel+LR on);
  * OCV modes = the generate_disparity node defaults (generate_disparity.cpp:100-112) and
  * ocv_compat = SGM_OCV_COMPAT_MELODIC (the OpenCV the reference's Dockerfile:1 ships).     */

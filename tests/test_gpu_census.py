@@ -391,3 +391,36 @@ def test_c5_tiled_exact_vs_full_frame(engine, synth, pkg):
     full = engine.match(left, right)
     tiled = engine.match_tiled_exact(left, right, 8)
     assert np.array_equal(tiled, full), f"{(tiled != full).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(speckle_window_size=30, speckle_range=2), dict(median=1)])
+@pytest.mark.parametrize("f32", [False, True])
+def test_registered_output_copy_out(engine, oracle, synth, pkg, kw, f32):
+    """sgm_host_register'ed outputs (the adapter's persistent disparity_lr): without post
+    filters the WTA runs in row bands whose rows are copied back while the next band is
+    matched; with them, one asynchronous copy after the match. Same result as the oracle and
+    as an unregistered output, in sgm_match (int16) and sgm_match_f32."""
+    h, w, D = 203, 300, 64
+    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=77)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, **kw)
+    engine.set_params(p)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    pad = 5
+    buf = np.full((h, w + pad), -7, np.float32 if f32 else np.int16)
+    out = buf[:, :w]
+    engine.host_register(buf)
+    try:
+        for _ in range(2):                                  # the second call reuses the registration
+            out[...] = -7
+            if f32:
+                engine.match_f32(left, right, out=out)
+            else:
+                engine._check(engine.lib.sgm_match(engine.h, left.ctypes.data, right.ctypes.data, w, h, w,
+                                                   out.ctypes.data, buf.shape[1]))
+            got = out.astype(np.float32) if f32 else out
+            assert np.array_equal(got, ref.astype(got.dtype))
+            assert (buf[:, w:] == -7).all()
+    finally:
+        engine.host_unregister(buf)
+    plain = engine.match_f32(left, right) if f32 else engine.match(left, right)
+    assert np.array_equal(plain, ref.astype(plain.dtype))

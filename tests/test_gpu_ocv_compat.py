@@ -104,11 +104,16 @@ def test_compat_overflow_frame(engine, oracle, pkg, mode, compat):
     _check(engine, oracle, p, left, right)
 
 
+@pytest.mark.parametrize("chain", ["sat2", "seq"])
 @pytest.mark.parametrize("compat", [0, 1, 2, 3])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_compat_cost_volume_overflow(engine, oracle, pkg, mode, compat):
+def test_compat_cost_volume_overflow(engine, oracle, pkg, monkeypatch, mode, compat, chain):
     """C' itself on the overflow frame (sgm_debug_ocv_cost): the wrapped scalar volume, or the
-    SIMD builds' saturated running sums from the sequential fallback kernels."""
+    SIMD builds' saturated running sums — from the vertical saturating update over the plain
+    horizontal sums (k_ocv_vsum_sat2, the default) and from the sequential chain it replaced
+    (SGM_OCV_SAT_SEQ=1)."""
+    if chain == "seq":
+        monkeypatch.setenv("SGM_OCV_SAT_SEQ", "1")
     left, right = _binary(64, 160, 1)
     p = pkg.default_params(mode, min_disparity=0, num_disparities=64, block_size=21, prefilter_cap=63, p1=50,
                            p2=3000, speckle_window_size=0, ocv_compat=compat)
@@ -118,6 +123,59 @@ def test_compat_cost_volume_overflow(engine, oracle, pkg, mode, compat):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} cells differ"
     if compat & 2:
         assert (ref == 32767).any()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_compat_cost_volume_saturating_hsum(engine, oracle, pkg, mode):
+    """A box wide enough for the SIMD horizontal running sums to saturate too (181 columns x
+    (2*63 + 63) > 32767): the sequential chain keeps the SIMD branch exact there."""
+    rng = np.random.default_rng(7)
+    left = (rng.integers(0, 2, (200, 260)) * 255).astype(np.uint8)
+    right = 255 - left
+    for compat in (2, 7):
+        p = pkg.default_params(mode, min_disparity=0, num_disparities=16, block_size=181, prefilter_cap=63, p1=50,
+                               p2=3000, speckle_window_size=0, ocv_compat=compat)
+        engine.set_params(p)
+        got = engine.ocv_cost(left, right)
+        ref = oracle.ocv_cost(to_oracle_params(oracle, p), left, right)
+        assert np.array_equal(got, ref), f"compat {compat}: {(got != ref).sum()} cells differ"
+        assert (ref == 32767).any()
+
+
+@pytest.fixture(scope="module")
+def full_overflow_pair():
+    """A capture-size (2448 x 2048) high-contrast frame: binary noise against its negative."""
+    return _binary(2048, 2448, 11)
+
+
+OVF_KW = dict(REF_KW, prefilter_cap=63, p2=4000, speckle_window_size=0)   # cfg maxima: C' passes 32767
+
+
+@pytest.mark.timeout(900)
+def test_compat_full_size_overflow_cost_volume(engine, oracle, pkg, full_overflow_pair):
+    """C' of a full 2448 x 2048 frame at the shipped geometry (min 147, D 480, block 21) in the
+    overflow regime (cap 63, P2 4000: box sums + P2 pass 32767), melodic and noetic (the SIMD
+    builds: saturating vertical sums) and the scalar build (wrapping), against the oracle."""
+    left, right = full_overflow_pair
+    sums = {}
+    for compat in (7, 2, 0):
+        p = pkg.default_params(0, ocv_compat=compat, **OVF_KW)
+        engine.set_params(p)
+        got = engine.ocv_cost(left, right)
+        ref = oracle.ocv_cost(to_oracle_params(oracle, p), left, right)
+        assert np.array_equal(got, ref), f"compat {compat}: {(got != ref).sum()} cells differ"
+        sums[compat] = int(ref[1:].astype(np.int64).sum())
+        if compat == 0:
+            assert (ref < 0).any()            # the scalar CostType wraps
+        del got, ref
+    assert sums[2] != sums[0]                  # the SIMD builds saturate instead
+
+
+@pytest.mark.timeout(900)
+def test_compat_full_size_overflow_frame(engine, oracle, pkg, full_overflow_pair):
+    """The same full-size overflow frame matched end to end under the default (melodic) build."""
+    left, right = full_overflow_pair
+    _check(engine, oracle, pkg.default_params(0, ocv_compat=7, **OVF_KW), left, right)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
