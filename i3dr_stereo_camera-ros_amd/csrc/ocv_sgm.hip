@@ -472,6 +472,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
                                                                  FuseGrid fg, int16_t* __restrict__ C)
 {
     static_assert(DPC / I * kFuseNX == kFuseThreads, "4 threads per staged column");
+    static_assert(R <= 21, "ring slots: cases 0..20 below");
     constexpr int TPC = DPC / I;
     extern __shared__ uint32_t lds_fuse[];
     const FuseGeo fz(DPC);
@@ -491,30 +492,57 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int xs = g.minX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
     const int xr0 = xs - g.minD - (d0 + DC - 1);             // right entry r <-> xr0 + r
     const size_t plane = (size_t)g.W * g.H;
-    auto stage = [&](int v, uint32_t* S) {                   // row of virtual row v, by waves 4-7
-        const int st = t - 256;
-        const int k_img = min(max(y0 - SH2 + v, 0), g.H - 1);
-        uint32_t* Lx = S;
-        uint16_t* Rh = (uint16_t*)(S + 6 * NX);
-        for (int i = st; i < 2 * NX; i += 256) {
-            const int c = i >= NX, k = i - c * NX;
-            const uint32_t w = bt[c * plane + (size_t)k_img * g.W + min(max(xs + k, 0), g.W - 1)];
-            uint32_t* o = Lx + 6 * k + 3 * c;
-            o[0] = (w & 0xFFu) * 0x10001u; o[1] = ((w >> 8) & 0xFFu) * 0x10001u; o[2] = ((w >> 16) & 0xFFu) * 0x10001u;
-        }
-        const int NRr = NX + DC - 1;
-        for (int i = st; i < 2 * NRr; i += 256) {
+    // staging, every thread: entries t and t + 512 of the row's 2 * NX left entries (first) and
+    // 2 * NRr right ones; the bt words of row v + 2 are loaded while row v + 1's are written to
+    // LDS, so a global load's latency spans a whole row phase
+    const int NRr = NX + DC - 1, NE = 2 * NX + 2 * NRr;
+    const uint32_t* src[2];
+    int dst[2];                                              // left: word offset; right: -1 - (c * NRr + r)
+    bool has[2];
+#pragma unroll
+    for (int e2 = 0; e2 < 2; e2++) {
+        const int e = t + e2 * kFuseThreads;
+        has[e2] = e < NE;
+        if (e < 2 * NX) {
+            const int c = e >= NX, k = e - c * NX;
+            src[e2] = bt + c * plane + min(max(xs + k, 0), g.W - 1);
+            dst[e2] = 6 * k + 3 * c;
+        } else {
+            const int i = min(e, NE - 1) - 2 * NX;
             const int c = i >= NRr, r = i - c * NRr;
-            const uint32_t w = bt[(2 + c) * plane + (size_t)k_img * g.W + min(max(xr0 + r, 0), g.W - 1)];
-            const int j = M - 1 - r;
-            uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
-            uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
-            const uint16_t v = w & 0xFF, lo = (w >> 8) & 0xFF, hi = (w >> 16) & 0xFF;
-            lo16[0] = v; lo16[2] = lo; lo16[4] = hi;
-            hi16[0] = v; hi16[2] = lo; hi16[4] = hi;
+            src[e2] = bt + (2 + c) * plane + min(max(xr0 + r, 0), g.W - 1);
+            dst[e2] = -1 - i;
+        }
+    }
+    uint32_t wst[2] = {0u, 0u};
+    auto stage_load = [&](int v) {
+        const size_t ro = (size_t)min(max(y0 - SH2 + v, 0), g.H - 1) * g.W;
+#pragma unroll
+        for (int e2 = 0; e2 < 2; e2++) wst[e2] = has[e2] ? src[e2][ro] : 0u;
+    };
+    auto stage_store = [&](uint32_t* S) {
+        uint16_t* Rh = (uint16_t*)(S + 6 * NX);
+#pragma unroll
+        for (int e2 = 0; e2 < 2; e2++) {
+            if (!has[e2]) continue;
+            const uint32_t w = wst[e2];
+            if (dst[e2] >= 0) {
+                uint32_t* o = S + dst[e2];
+                o[0] = (w & 0xFFu) * 0x10001u; o[1] = ((w >> 8) & 0xFFu) * 0x10001u; o[2] = ((w >> 16) & 0xFFu) * 0x10001u;
+            } else {
+                const int i = -1 - dst[e2], c = i >= NRr, r = i - c * NRr;
+                const int j = M - 1 - r;
+                uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
+                uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
+                const uint16_t v = w & 0xFF, lo = (w >> 8) & 0xFF, hi = (w >> 16) & 0xFF;
+                lo16[0] = v; lo16[2] = lo; lo16[4] = hi;
+                hi16[0] = v; hi16[2] = lo; hi16[4] = hi;
+            }
         }
     };
-    // P + ring + V: staged column kc, pairs tq*I .. tq*I + I - 1
+    // P + ring + V: staged column kc, pairs tq*I .. tq*I + I - 1; the last R rows of P in
+    // registers, slot v mod R picked by a uniform switch (static register indices, one copy of
+    // the row code)
     const int kc = t / TPC, tq = t % TPC;
     uint32_t ring[I][R];
     uint32_t Vs[I];
@@ -522,14 +550,15 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     for (int q = 0; q < I; q++) {
         Vs[q] = 0;
 #pragma unroll
-        for (int s = 0; s < R; s++) ring[q][s] = 0;
+        for (int s2 = 0; s2 < R; s2++) ring[q][s2] = 0;
     }
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
-    // box: thread (segment, pair) of waves 0-3
+    // box: thread (segment, pair), every thread
     const int nout = min(XB, g.width1 - x0);
     const int klo = max(SW2 - x0, 0), khi = min(g.width1 - 1 - x0 + SW2, NX - 1);
-    constexpr int NSEG = 256 / DPC;
+    const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
+    constexpr int NSEG = kFuseThreads / DPC;
     const int bp = t % DPC, bseg = t / DPC;
     const int seglen = (nout + NSEG - 1) / NSEG;
     const int xa = bseg * seglen, xb = min(xa + seglen, nout);
@@ -538,76 +567,91 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const u16x2_t p2v = {(unsigned short)g.P2, (unsigned short)g.P2};
     uint32_t* C32 = (uint32_t*)C;
     const size_t rowC = (size_t)g.width1 * g.D / 2;         // u32 per C' row
-    auto box = [&](int y, const uint32_t* V, bool tail) {   // output row y (waves 0-3)
-        if (xa >= xb) return;
-        const uint32_t* Vp = V + bp;
-        auto rd = [&](int k) { return __builtin_bit_cast(u16x2_t, Vp[min(max(k, klo), khi) * DPC]); };
-        u16x2_t sum = {0, 0};
-        for (int u = 0; u <= 2 * SW2; u++) sum += rd(xa + u);
-        uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * g.D + d0) / 2 + bp;
-        for (int xo = xa; xo < xb; xo++) {
-            if (xo > xa) sum += rd(xo + 2 * SW2) - rd(xo - 1);
-            if (!(col0 && xo == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
-            const uint32_t c = __builtin_bit_cast(uint32_t, sum + p2v);
-            o[0] = c;
-            if (tail)                                        // OpenCV's bottom rows: never recomputed
-                for (int yy = y + 1; yy < g.H; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? g.P2 * 0x10001u : c;
-            o += g.D / 2;
-        }
-    };
-    if (t >= 256) stage(0, S0);
-    __syncthreads();
     const bool last_band = y1 == fg.ncomp;
-    for (int vb = 0; vb <= nv; vb += R) {
-        static_for<0, R>([&](auto jj) {
-            constexpr int s = decltype(jj)::value;
-            const int v = vb + s;
-            if (v > nv) return;                              // uniform
-            uint32_t* S = S0 + (v & 1) * fz.stage_words();
-            if (v < nv) {
-                const uint32_t* Lk = S + 6 * kc;
-                u16x2_t u[2], ulo[2], uhi[2];
+    stage_load(0);
+    stage_store(S0);
+    if (1 < nv) stage_load(1);
+    __syncthreads();
+    int slot = 0;
+    for (int v = 0; v <= nv; v++) {
+        uint32_t* S = S0 + (v & 1) * fz.stage_words();
+        if (v < nv) {
+            const uint32_t* Lk = S + 6 * kc;
+            u16x2_t u[2], ulo[2], uhi[2];
 #pragma unroll
-                for (int c = 0; c < 2; c++) { u[c] = wd(Lk, 3 * c); ulo[c] = wd(Lk, 3 * c + 1); uhi[c] = wd(Lk, 3 * c + 2); }
-                const int j0 = M - DC - kc + 2 * tq * I;
-                const uint32_t* Rk = S + 6 * NX + 7 * ((j0 & 1) * MH + (j0 >> 1));
-                uint32_t* Vout = V0 + (v & 1) * NX * DPC + kc * DPC + tq * I;
+            for (int c = 0; c < 2; c++) { u[c] = wd(Lk, 3 * c); ulo[c] = wd(Lk, 3 * c + 1); uhi[c] = wd(Lk, 3 * c + 2); }
+            const int j0 = M - DC - kc + 2 * tq * I;
+            const uint32_t* Rk = S + 6 * NX + 7 * ((j0 & 1) * MH + (j0 >> 1));
+            uint32_t P[I];
+#pragma unroll
+            for (int q = 0; q < I; q++) {
+                u16x2_t m[2];
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const u16x2_t vv = wd(Rk, 7 * q + 3 * c), v0 = wd(Rk, 7 * q + 3 * c + 1), v1 = wd(Rk, 7 * q + 3 * c + 2);
+                    const u16x2_t c0 = __builtin_elementwise_max(sat(u[c], v1), sat(v0, u[c]));
+                    const u16x2_t c1 = __builtin_elementwise_max(sat(vv, uhi[c]), sat(ulo[c], vv));
+                    m[c] = __builtin_elementwise_min(c0, c1);
+                }
+                P[q] = __builtin_bit_cast(uint32_t, m[0] + (m[1] >> (u16x2_t){2, 2}));
+            }
+            auto upd = [&](auto ss) {
+                constexpr int s2 = decltype(ss)::value;
 #pragma unroll
                 for (int q = 0; q < I; q++) {
-                    u16x2_t m[2];
-#pragma unroll
-                    for (int c = 0; c < 2; c++) {
-                        const u16x2_t vv = wd(Rk, 7 * q + 3 * c), v0 = wd(Rk, 7 * q + 3 * c + 1), v1 = wd(Rk, 7 * q + 3 * c + 2);
-                        const u16x2_t c0 = __builtin_elementwise_max(sat(u[c], v1), sat(v0, u[c]));
-                        const u16x2_t c1 = __builtin_elementwise_max(sat(vv, uhi[c]), sat(ulo[c], vv));
-                        m[c] = __builtin_elementwise_min(c0, c1);
-                    }
-                    const uint32_t P = __builtin_bit_cast(uint32_t, m[0] + (m[1] >> (u16x2_t){2, 2}));
-                    Vs[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, Vs[q]) + __builtin_bit_cast(u16x2_t, P) -
-                                                         __builtin_bit_cast(u16x2_t, ring[q][s]));
-                    ring[q][s] = P;
+                    Vs[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, Vs[q]) + __builtin_bit_cast(u16x2_t, P[q]) -
+                                                         __builtin_bit_cast(u16x2_t, ring[q][s2]));
+                    ring[q][s2] = P[q];
                 }
-                if (v >= 2 * SH2) {
-                    if constexpr (I == 4) {
-                        *(uint4*)Vout = make_uint4(Vs[0], Vs[1], Vs[2], Vs[3]);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
-                    }
-                }
+            };
+            switch (slot) {
+#define SGM_RING_CASE(n) case n: if constexpr (n < R) upd(std::integral_constant<int, n>{}); break;
+            SGM_RING_CASE(0) SGM_RING_CASE(1) SGM_RING_CASE(2) SGM_RING_CASE(3) SGM_RING_CASE(4) SGM_RING_CASE(5)
+            SGM_RING_CASE(6) SGM_RING_CASE(7) SGM_RING_CASE(8) SGM_RING_CASE(9) SGM_RING_CASE(10) SGM_RING_CASE(11)
+            SGM_RING_CASE(12) SGM_RING_CASE(13) SGM_RING_CASE(14) SGM_RING_CASE(15) SGM_RING_CASE(16)
+            SGM_RING_CASE(17) SGM_RING_CASE(18) SGM_RING_CASE(19) SGM_RING_CASE(20)
+#undef SGM_RING_CASE
+            default: break;
             }
-            if (t < 256) {
-                if (v >= 1 && v - 1 >= 2 * SH2) {
-                    const int y = y0 + (v - 1) - 2 * SH2;
-                    box(y, V0 + ((v - 1) & 1) * NX * DPC, last_band && y == fg.ncomp - 1);
-                }
-            } else if (v + 1 < nv) {
-                stage(v + 1, S0 + ((v + 1) & 1) * fz.stage_words());
+            slot = slot + 1 == R ? 0 : slot + 1;
+            if (v >= 2 * SH2) {
+                uint32_t* Vout = V0 + (v & 1) * NX * DPC + kc * DPC + tq * I;
+#pragma unroll
+                for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
             }
-            __syncthreads();
-        });
+        }
+        if (v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {         // the box of row v - 1
+            const int y = y0 + (v - 1) - 2 * SH2;
+            const bool tail = last_band && y == fg.ncomp - 1;
+            const uint32_t* Vp = V0 + ((v - 1) & 1) * NX * DPC + bp;
+            auto slide = [&](auto clampit) {
+                auto rd = [&](int k) {
+                    if constexpr (decltype(clampit)::value) k = min(max(k, klo), khi);
+                    return __builtin_bit_cast(u16x2_t, Vp[k * DPC]);
+                };
+                u16x2_t sum = {0, 0};
+                for (int u2 = 0; u2 <= 2 * SW2; u2++) sum += rd(xa + u2);
+                uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * g.D + d0) / 2 + bp;
+                for (int xo = xa; xo < xb; xo++) {
+                    if (xo > xa) sum += rd(xo + 2 * SW2) - rd(xo - 1);
+                    if (!(col0 && xo == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
+                    const uint32_t c = __builtin_bit_cast(uint32_t, sum + p2v);
+                    o[0] = c;
+                    if (tail)                                // OpenCV's bottom rows: never recomputed
+                        for (int yy = y + 1; yy < g.H; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? g.P2 * 0x10001u : c;
+                    o += g.D / 2;
+                }
+            };
+            if (edge) slide(std::true_type{});
+            else slide(std::false_type{});
+        }
+        if (v + 1 < nv) {
+            stage_store(S0 + ((v + 1) & 1) * fz.stage_words());
+            if (v + 2 < nv) stage_load(v + 2);
+        }
+        __syncthreads();
     }
-    if (g.wide == 2 && g.ovf && t < 256) {
+    if (g.wide == 2 && g.ovf) {
         const int m = max((int)bmax[0], (int)bmax[1]);
         const bool ovf = m > g.ovf_thr - g.P2;
         const uint64_t b = __ballot(ovf);
@@ -630,7 +674,11 @@ __host__ inline bool ocv_cost_fusable(const Geom& g)
 {
     const long long B = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63);
     const char* e = std::getenv("SGM_OCV_FUSED");
-    return g.SH2 <= 10 && g.SW2 <= 10 && B <= 65535 && g.width1 > 0 && e && std::atoi(e) != 0;
+    // default: frames with enough tiles x bands to fill the chip, and boxes up to 9 x 9 (wider
+    // ones need long horizontal windows that the two-kernel form slides more cheaply: the
+    // shipped block-21 config measured 5.2 fused vs 3.8 ms, profiles/r04_ocv_cost_ab.jsonl)
+    const bool dflt = (double)g.width1 * g.H * g.D >= 1e8 && g.SH2 <= 4;
+    return g.SH2 <= 10 && g.SW2 <= 10 && B <= 65535 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
 }
 
 // The SIMD_SAT flagged frames whose horizontal sums cannot saturate: when
@@ -1415,18 +1463,33 @@ static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <
 // over it, by kernels that return at once on the other frames: the vertical SIMD update over
 // the plain horizontal sums (k_ocv_vsum_sat2) when those cannot saturate, else the sequential
 // chain (pixel costs -> bufA, horizontal sums -> bufB, C' -> bufA).
+// Disparity pairs per block row (DC = 2 * DPC disparities): 32 only for R <= 9 (its I = 8
+// pairs per thread keep 8 R-slot rings in registers), else 16, or 8 (I = 2: 95 VGPRs at R = 21
+// against 165 for 16, i.e. two blocks per CU instead of one); SGM_FUSE_DPC forces one.
+static int fuse_dpc(const Geom& g)
+{
+    const int R = 2 * g.SH2 + 1;
+    int dpc = (R <= 9 && g.D % 64 == 0) ? 32 : g.D % 32 == 0 ? 16 : 8;
+    if (const char* e = std::getenv("SGM_FUSE_DPC")) {
+        const int f = std::atoi(e);
+        if ((f == 32 && R <= 9 && g.D % 64 == 0) || (f == 16 && g.D % 32 == 0) || f == 8) dpc = f;
+    }
+    return dpc;
+}
+
 template <int R>
 static void launch_cost_fused_r(const uint32_t* bt, const Geom& g, int fullDP, const FuseGrid& fg, int16_t* C,
                                 hipStream_t st)
 {
     const dim3 grid(fg.per_xcd * 8), block(kFuseThreads);
+    const int dpc = fuse_dpc(g);
     if constexpr (R <= 9) {
-        if (g.D % 64 == 0) {
+        if (dpc == 32) {
             hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8>), grid, block, FuseGeo(32).lds_bytes(32), st, bt, g, fullDP, fg, C);
             return;
         }
     }
-    if (g.D % 32 == 0)
+    if (dpc == 16)
         hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4>), grid, block, FuseGeo(16).lds_bytes(16), st, bt, g, fullDP, fg, C);
     else
         hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2>), grid, block, FuseGeo(8).lds_bytes(8), st, bt, g, fullDP, fg, C);
@@ -1435,7 +1498,7 @@ static void launch_cost_fused_r(const uint32_t* bt, const Geom& g, int fullDP, c
 static FuseGrid fuse_grid(const Geom& g)
 {
     FuseGrid fg{};
-    const int dpc = (2 * g.SH2 + 1 <= 9 && g.D % 64 == 0) ? 32 : g.D % 32 == 0 ? 16 : 8;
+    const int dpc = fuse_dpc(g);
     const int XB = fuse_xb(g);
     fg.strips = (g.width1 + XB - 1) / XB;
     fg.chunks = g.D / (2 * dpc);
@@ -1443,7 +1506,7 @@ static FuseGrid fuse_grid(const Geom& g)
     const long long tiles = (long long)fg.strips * fg.chunks;
     const char* e = std::getenv("SGM_FUSE_ROWS");
     fg.band_rows = e ? std::max(std::atoi(e), 1)
-                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
+                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 511) / 512);
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;
