@@ -820,7 +820,9 @@ int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H,
     }
     // lanes whose workspaces take more than a quarter of the device are not kept past the call
     // (a later call on h, or another handle, may need that memory): the call waits for them
-    if ((size_t)(S - 1) * l0.total > total_b / 4) {
+    // (SGM_OCV_KEEP_LANES=1 keeps them: the A/B of profiles/r04_ocv_lanes_ab.jsonl)
+    const char* keep = std::getenv("SGM_OCV_KEEP_LANES");
+    if ((size_t)(S - 1) * l0.total > total_b / 4 && !(keep && std::atoi(keep))) {
         for (int s = 1; s < S; s++) {
             sgm_handle* q = h->par[s - 1];
             HIP_TRY(hipStreamSynchronize(q->stream), "hipStreamSynchronize");
@@ -853,6 +855,11 @@ bool host_pinned(const void* p)
 // WTA runs in kOutChunks row bands and band i's rows go back on the `down` stream while band
 // i + 1 is matched, so only the last band's copy adds to the call.
 constexpr int kOutChunks = 4;
+int out_chunks()
+{
+    const char* e = std::getenv("SGM_OUT_CHUNKS");          // measurement knob: 1 = one copy after the match
+    return e ? std::min(std::max(std::atoi(e), 1), kOutChunks) : kOutChunks;
+}
 
 int ensure_down(sgm_handle* h)
 {
@@ -897,11 +904,14 @@ int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, 
         return SGM_OK;
     };
     const bool chunked = h->params.mode == SGM_MODE_CENSUS8 && !use_median(h->params) &&
-                         h->params.speckle_window_size <= 0 && g.width1 > 0 && H >= 2 * kOutChunks && host_pinned(out);
+                         h->params.speckle_window_size <= 0 && g.width1 > 0 && H >= 2 * kOutChunks && out_chunks() > 1 &&
+                         host_pinned(out);
+    if (std::getenv("SGM_IO_TRACE")) std::fprintf(stderr, "[sgm io] match_host: pinned out %d, chunked %d\n",
+                                                  (int)host_pinned(out), (int)chunked);
     if (chunked) {
         if ((rc = ensure_down(h))) return rc;
         RowsHook hook;
-        hook.chunks = kOutChunks;
+        hook.chunks = out_chunks();
         int chunk = 0;
         hook.done = [&](int y0, int y1) { return copy_out(y0, y1, h->down, chunk++); };
         rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W, &hook);
