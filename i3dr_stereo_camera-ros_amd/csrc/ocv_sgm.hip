@@ -466,6 +466,7 @@ struct FuseGeo {
 };
 struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
+    int box_segs;            // output segments per disparity pair (the box threads: box_segs * DPC)
 };
 template <int R, int DPC, int I>
 __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
@@ -558,10 +559,10 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int nout = min(XB, g.width1 - x0);
     const int klo = max(SW2 - x0, 0), khi = min(g.width1 - 1 - x0 + SW2, NX - 1);
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
-    constexpr int NSEG = kFuseThreads / DPC;
+    const int NSEG = fg.box_segs;                            // <= kFuseThreads / DPC
     const int bp = t % DPC, bseg = t / DPC;
     const int seglen = (nout + NSEG - 1) / NSEG;
-    const int xa = bseg * seglen, xb = min(xa + seglen, nout);
+    const int xa = bseg < NSEG ? bseg * seglen : nout, xb = min(xa + seglen, nout);
     u16x2_t bmax = {0, 0};                                   // flag: the largest box sum seen
     const bool col0 = (g.compat & SGM_OCV_COL0_LEGACY) && x0 == 0;
     const u16x2_t p2v = {(unsigned short)g.P2, (unsigned short)g.P2};
@@ -1510,6 +1511,10 @@ static FuseGrid fuse_grid(const Geom& g)
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;
+    // box segments per pair: every thread by default (each slides its window over
+    // seglen = XB / segs outputs after a 2*SW2+1 read start); SGM_FUSE_BOXSEG for fewer, longer ones
+    fg.box_segs = kFuseThreads / dpc;
+    if (const char* b = std::getenv("SGM_FUSE_BOXSEG")) fg.box_segs = std::min(std::max(std::atoi(b), 1), kFuseThreads / dpc);
     return fg;
 }
 

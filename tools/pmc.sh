@@ -7,7 +7,7 @@ set -u
 D=${PMC_DIR:-gpurun_out/pmc}
 mkdir -p $D
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 1 --warmup 1 --frames 32 --no-cpu-baseline ${BENCH_ARGS:-}"
+CMD="python3 bench.py --steps 1 --warmup 1 --frames 32 --no-cpu-baseline --no-c5 ${BENCH_ARGS:-}"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \

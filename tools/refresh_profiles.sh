@@ -30,7 +30,7 @@ step c2_bench 600 python3 bench.py --config c2 --no-cpu-baseline
 for cfg in c3 c2; do
   rm -rf $O/prof_$cfg
   step ${cfg}_rocprof 600 rocprofv3 --kernel-trace --stats -d $O/prof_$cfg -o run --output-format csv -- \
-      python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline
+      python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline --no-c5
   python3 tools/prof_compare.py "$(find $O/prof_$cfg -name '*kernel_trace.csv' | head -1)" \
       $O/${cfg}_rocprof.log > $O/${cfg}_prof_vs_bench.txt || exit 1
   cp "$(find $O/prof_$cfg -name '*kernel_stats.csv' | head -1)" $O/${cfg}_kernel_stats.csv
