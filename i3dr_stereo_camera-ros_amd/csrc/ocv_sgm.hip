@@ -493,53 +493,39 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int xs = g.minX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
     const int xr0 = xs - g.minD - (d0 + DC - 1);             // right entry r <-> xr0 + r
     const size_t plane = (size_t)g.W * g.H;
-    // staging, every thread: entries t and t + 512 of the row's 2 * NX left entries (first) and
-    // 2 * NRr right ones; the bt words of row v + 2 are loaded while row v + 1's are written to
-    // LDS, so a global load's latency spans a whole row phase
-    const int NRr = NX + DC - 1, NE = 2 * NX + 2 * NRr;
-    const uint32_t* src[2];
-    int dst[2];                                              // left: word offset; right: -1 - (c * NRr + r)
-    bool has[2];
-#pragma unroll
-    for (int e2 = 0; e2 < 2; e2++) {
-        const int e = t + e2 * kFuseThreads;
-        has[e2] = e < NE;
-        if (e < 2 * NX) {
-            const int c = e >= NX, k = e - c * NX;
-            src[e2] = bt + c * plane + min(max(xs + k, 0), g.W - 1);
-            dst[e2] = 6 * k + 3 * c;
-        } else {
-            const int i = min(e, NE - 1) - 2 * NX;
-            const int c = i >= NRr, r = i - c * NRr;
-            src[e2] = bt + (2 + c) * plane + min(max(xr0 + r, 0), g.W - 1);
-            dst[e2] = -1 - i;
-        }
-    }
-    uint32_t wst[2] = {0u, 0u};
+    // staging (waves 4-7, beside the box of waves 0-3): entry st of the 2 * NX left entries (one
+    // each) and entries st, st + 256 of the 2 * NRr right ones; the bt words of row v + 2 are
+    // loaded while row v + 1's are written to LDS, so a global load's latency spans a whole phase
+    const int st = t - 256;
+    const int NRr = NX + DC - 1;
+    const int cl = st >= NX, kl = st - cl * NX;
+    const int cr0 = st >= NRr, r0 = st - cr0 * NRr;
+    const bool has1 = st + 256 < 2 * NRr;
+    const int cr1 = st + 256 >= NRr, r1 = st + 256 - cr1 * NRr;
+    const uint32_t* btL = bt + cl * plane + min(max(xs + kl, 0), g.W - 1);
+    const uint32_t* btR0 = bt + (2 + cr0) * plane + min(max(xr0 + r0, 0), g.W - 1);
+    const uint32_t* btR1 = bt + (2 + cr1) * plane + min(max(xr0 + r1, 0), g.W - 1);
+    uint32_t wl = 0, wr0 = 0, wr1 = 0;
     auto stage_load = [&](int v) {
         const size_t ro = (size_t)min(max(y0 - SH2 + v, 0), g.H - 1) * g.W;
-#pragma unroll
-        for (int e2 = 0; e2 < 2; e2++) wst[e2] = has[e2] ? src[e2][ro] : 0u;
+        wl = btL[ro];
+        wr0 = btR0[ro];
+        wr1 = has1 ? btR1[ro] : 0u;
+    };
+    auto put_right = [&](uint16_t* Rh, int c, int r, uint32_t w) {
+        const int j = M - 1 - r;
+        uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
+        uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
+        const uint16_t v = w & 0xFF, lo = (w >> 8) & 0xFF, hi = (w >> 16) & 0xFF;
+        lo16[0] = v; lo16[2] = lo; lo16[4] = hi;
+        hi16[0] = v; hi16[2] = lo; hi16[4] = hi;
     };
     auto stage_store = [&](uint32_t* S) {
+        uint32_t* o = S + 6 * kl + 3 * cl;
+        o[0] = (wl & 0xFFu) * 0x10001u; o[1] = ((wl >> 8) & 0xFFu) * 0x10001u; o[2] = ((wl >> 16) & 0xFFu) * 0x10001u;
         uint16_t* Rh = (uint16_t*)(S + 6 * NX);
-#pragma unroll
-        for (int e2 = 0; e2 < 2; e2++) {
-            if (!has[e2]) continue;
-            const uint32_t w = wst[e2];
-            if (dst[e2] >= 0) {
-                uint32_t* o = S + dst[e2];
-                o[0] = (w & 0xFFu) * 0x10001u; o[1] = ((w >> 8) & 0xFFu) * 0x10001u; o[2] = ((w >> 16) & 0xFFu) * 0x10001u;
-            } else {
-                const int i = -1 - dst[e2], c = i >= NRr, r = i - c * NRr;
-                const int j = M - 1 - r;
-                uint16_t* lo16 = Rh + 2 * (7 * ((j & 1) * MH + (j >> 1)) + 3 * c);
-                uint16_t* hi16 = Rh + 2 * (7 * (((j - 1) & 1) * MH + ((j - 1) >> 1)) + 3 * c) + 1;
-                const uint16_t v = w & 0xFF, lo = (w >> 8) & 0xFF, hi = (w >> 16) & 0xFF;
-                lo16[0] = v; lo16[2] = lo; lo16[4] = hi;
-                hi16[0] = v; hi16[2] = lo; hi16[4] = hi;
-            }
-        }
+        put_right(Rh, cr0, r0, wr0);
+        if (has1) put_right(Rh, cr1, r1, wr1);
     };
     // P + ring + V: staged column kc, pairs tq*I .. tq*I + I - 1; the last R rows of P in
     // registers, slot v mod R picked by a uniform switch (static register indices, one copy of
@@ -555,11 +541,11 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     }
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
-    // box: thread (segment, pair), every thread
+    // box: thread (segment, pair) of waves 0-3
     const int nout = min(XB, g.width1 - x0);
     const int klo = max(SW2 - x0, 0), khi = min(g.width1 - 1 - x0 + SW2, NX - 1);
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
-    const int NSEG = fg.box_segs;                            // <= kFuseThreads / DPC
+    const int NSEG = fg.box_segs;                            // <= 256 / DPC
     const int bp = t % DPC, bseg = t / DPC;
     const int seglen = (nout + NSEG - 1) / NSEG;
     const int xa = bseg < NSEG ? bseg * seglen : nout, xb = min(xa + seglen, nout);
@@ -569,9 +555,11 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     uint32_t* C32 = (uint32_t*)C;
     const size_t rowC = (size_t)g.width1 * g.D / 2;         // u32 per C' row
     const bool last_band = y1 == fg.ncomp;
-    stage_load(0);
-    stage_store(S0);
-    if (1 < nv) stage_load(1);
+    if (t >= 256) {
+        stage_load(0);
+        stage_store(S0);
+        if (1 < nv) stage_load(1);
+    }
     __syncthreads();
     int slot = 0;
     for (int v = 0; v <= nv; v++) {
@@ -621,7 +609,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
                 for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
             }
         }
-        if (v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {         // the box of row v - 1
+        if (t < 256 && v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {   // the box of row v - 1
             const int y = y0 + (v - 1) - 2 * SH2;
             const bool tail = last_band && y == fg.ncomp - 1;
             const uint32_t* Vp = V0 + ((v - 1) & 1) * NX * DPC + bp;
@@ -646,13 +634,13 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
             if (edge) slide(std::true_type{});
             else slide(std::false_type{});
         }
-        if (v + 1 < nv) {
+        if (t >= 256 && v + 1 < nv) {
             stage_store(S0 + ((v + 1) & 1) * fz.stage_words());
             if (v + 2 < nv) stage_load(v + 2);
         }
         __syncthreads();
     }
-    if (g.wide == 2 && g.ovf) {
+    if (g.wide == 2 && g.ovf && t < 256) {
         const int m = max((int)bmax[0], (int)bmax[1]);
         const bool ovf = m > g.ovf_thr - g.P2;
         const uint64_t b = __ballot(ovf);
@@ -1507,14 +1495,14 @@ static FuseGrid fuse_grid(const Geom& g)
     const long long tiles = (long long)fg.strips * fg.chunks;
     const char* e = std::getenv("SGM_FUSE_ROWS");
     fg.band_rows = e ? std::max(std::atoi(e), 1)
-                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 511) / 512);
+                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;
     // box segments per pair: every thread by default (each slides its window over
     // seglen = XB / segs outputs after a 2*SW2+1 read start); SGM_FUSE_BOXSEG for fewer, longer ones
-    fg.box_segs = kFuseThreads / dpc;
-    if (const char* b = std::getenv("SGM_FUSE_BOXSEG")) fg.box_segs = std::min(std::max(std::atoi(b), 1), kFuseThreads / dpc);
+    fg.box_segs = 256 / dpc;
+    if (const char* b = std::getenv("SGM_FUSE_BOXSEG")) fg.box_segs = std::min(std::max(std::atoi(b), 1), 256 / dpc);
     return fg;
 }
 

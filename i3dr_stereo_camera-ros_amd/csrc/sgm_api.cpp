@@ -14,7 +14,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -472,17 +471,9 @@ bool ocv_vwta_on(const Geom& g, int fullDP)
     return (double)g.width1 * g.H * g.D >= (fullDP ? 2.0e8 : 1.0e9);
 }
 
-// Rows of the output that are final, in order, while the pipeline is still running: the census
-// WTA in `chunks` row bands (no post filter follows it), `done(y0, y1)` called after each band's
-// launch is queued on h->stream (match_host's chunked copy-out).
-struct RowsHook {
-    int chunks = 1;
-    std::function<int(int, int)> done;
-};
-
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
-                 int16_t* dOut, size_t out_stride, const RowsHook* hook = nullptr)
+                 int16_t* dOut, size_t out_stride)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
@@ -515,23 +506,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
-        if (hook && hook->chunks > 1 && !med && p.speckle_window_size <= 0) {
-            // one WTA launch per row band (a row's WTA, disp2 and LR need only its own row)
-            const size_t vrow = (size_t)g.width1 * g.D;
-            for (int c = 0; c < hook->chunks; c++) {
-                const int y0 = (int)((long long)c * g.H / hook->chunks), y1 = (int)((long long)(c + 1) * g.H / hook->chunks);
-                if (y1 <= y0) continue;
-                Geom gc = g;
-                gc.H = y1 - y0;
-                sgm::WtaFrames wc = wf;
-                wc.vols[0] = vols + (size_t)y0 * vrow;
-                wc.out[0] = dst + (size_t)y0 * dst_stride;
-                HIP_TRY(sgm::launch_census_wta(wc, l.vol_bytes, gc, dst_stride, st), "wta");
-                if (int r = hook->done(y0, y1)) return r;
-            }
-        } else {
-            HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
-        }
+        HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
@@ -840,40 +815,14 @@ int run_batch_ocv(sgm_handle* h, const Layout& l0, const Geom& g0, int W, int H,
 // matcherOpenCVSGBM.cpp:17-44 (compute, then convertTo CV_32FC1), called per frame from
 // generate_disparity.cpp:334-368. Every copy is one 2-D DMA between the caller's (pageable)
 // rows and the workspace: measured on the MI355X box (tools/probe/host_copy.cpp,
-// profiles/r03_host_copy.txt), a pageable 1920x1080 H2D takes 58 us against 42 us of CPU
+// profiles/r04_host_copy.txt), a pageable 1920x1080 H2D takes 58 us against 42 us of CPU
 // packing + 45 us of pinned DMA, and the 8.3 MB float D2H runs at the same 53 GB/s into
 // pageable or pinned memory — staging buffers would only add copies.
-// Is [p, p + bytes) page-locked host memory (sgm_host_register / hipHostMalloc)?
-bool host_pinned(const void* p)
-{
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
-    return a.type == hipMemoryTypeHost;
-}
-
-// Rows per copy-out chunk of a pinned host output (census frames without post filters): the
-// WTA runs in kOutChunks row bands and band i's rows go back on the `down` stream while band
-// i + 1 is matched, so only the last band's copy adds to the call.
-constexpr int kOutChunks = 4;
-int out_chunks()
-{
-    const char* e = std::getenv("SGM_OUT_CHUNKS");          // measurement knob: 1 = one copy after the match
-    return e ? std::min(std::max(std::atoi(e), 1), kOutChunks) : kOutChunks;
-}
-
-int ensure_down(sgm_handle* h)
-{
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-    if (!h->down) HIP_TRY(hipStreamCreateWithPriority(&h->down, hipStreamNonBlocking, hi), "hipStreamCreate");
-    while (h->io_ev.size() < (size_t)kOutChunks) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-        h->io_ev.push_back(e);
-    }
-    return SGM_OK;
-}
-
+// A caller may page-lock `out` with sgm_host_register (the adapter does, for its persistent
+// disparity_lr): the D2H then needs no runtime staging, 1920x1080 f32 forwardMatch 1.95-1.97
+// vs 1.97-1.99 ms pageable (profiles/r04_host_copy_ab.jsonl). Copying the rows back in 4 bands
+// behind a banded WTA measured no gain (1.97-2.00 ms): a quarter-frame WTA launch (270 row
+// workgroups) runs below the full launch's efficiency by about what the overlap saves.
 int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, size_t stride, void* out,
                size_t out_stride, bool f32)
 {
@@ -887,41 +836,14 @@ int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, 
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, st), "H2D L");
     HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
     int16_t* d16 = (int16_t*)(ws + l.out);
-    float* df = (float*)(ws + l.outf);
-    const void* dsrc = f32 ? (const void*)df : (const void*)d16;
-    // copy rows [y0, y1) out (y0 < 0: the whole frame) on stream `cs`
-    auto copy_out = [&](int y0, int y1, hipStream_t cs, int chunk) -> int {
-        if (y0 < 0) { y0 = 0; y1 = H; }
-        if (f32) HIP_TRY(sgm::launch_to_f32(d16 + (size_t)y0 * W, W, df + (size_t)y0 * W, W, W, y1 - y0, st), "to_f32");
-        if (cs != st) {
-            hipEvent_t ev = h->io_ev[chunk % kOutChunks];
-            HIP_TRY(hipEventRecord(ev, st), "hipEventRecord");
-            HIP_TRY(hipStreamWaitEvent(cs, ev, 0), "hipStreamWaitEvent");
-        }
-        HIP_TRY(hipMemcpy2DAsync((char*)out + (size_t)y0 * out_stride * es, out_stride * es,
-                                 (const char*)dsrc + (size_t)y0 * W * es, W * es, W * es, y1 - y0,
-                                 hipMemcpyDeviceToHost, cs), "D2H");
-        return SGM_OK;
-    };
-    const bool chunked = h->params.mode == SGM_MODE_CENSUS8 && !use_median(h->params) &&
-                         h->params.speckle_window_size <= 0 && g.width1 > 0 && H >= 2 * kOutChunks && out_chunks() > 1 &&
-                         host_pinned(out);
-    if (std::getenv("SGM_IO_TRACE")) std::fprintf(stderr, "[sgm io] match_host: pinned out %d, chunked %d\n",
-                                                  (int)host_pinned(out), (int)chunked);
-    if (chunked) {
-        if ((rc = ensure_down(h))) return rc;
-        RowsHook hook;
-        hook.chunks = out_chunks();
-        int chunk = 0;
-        hook.done = [&](int y0, int y1) { return copy_out(y0, y1, h->down, chunk++); };
-        rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W, &hook);
-        if (rc) { (void)hipStreamSynchronize(st); (void)hipStreamSynchronize(h->down); return rc; }
-        HIP_TRY(hipStreamSynchronize(h->down), "sync down");
-    } else {
-        rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
-        if (rc) return rc;
-        if ((rc = copy_out(-1, -1, st, 0))) return rc;
+    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
+    if (rc) return rc;
+    const void* dsrc = d16;
+    if (f32) {
+        HIP_TRY(sgm::launch_to_f32(d16, W, (float*)(ws + l.outf), W, W, H, st), "to_f32");
+        dsrc = ws + l.outf;
     }
+    HIP_TRY(hipMemcpy2DAsync(out, out_stride * es, dsrc, W * es, W * es, H, hipMemcpyDeviceToHost, st), "D2H");
     HIP_TRY(hipStreamSynchronize(st), "sync");
     return mark_done(h, st);
 }

@@ -109,11 +109,9 @@ int  sgm_device_count(void);
 int  sgm_create(sgm_handle** out, int device);
 void sgm_destroy(sgm_handle* h);
 
-/* Page-lock a caller's host buffer (hipHostRegister) for as long as it stays registered. A
- * registered output of sgm_match / sgm_match_f32 is filled by asynchronous copies that overlap
- * the end of the match (census frames without post filters: the WTA runs in row bands and each
- * band's rows go back while the next is matched); unregistered memory takes one synchronous copy
- * after the match. The caller must unregister a buffer before freeing it (the MatcherHIPSGM
+/* Page-lock a caller's host buffer (hipHostRegister) for as long as it stays registered: a
+ * registered output of sgm_match / sgm_match_f32 is copied back by DMA without the runtime's
+ * pageable staging. The caller must unregister a buffer before freeing it (the MatcherHIPSGM
  * adapter registers its persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat).      */
 int  sgm_host_register(sgm_handle* h, void* ptr, size_t bytes);
 int  sgm_host_unregister(sgm_handle* h, void* ptr);

@@ -396,10 +396,10 @@ def test_c5_tiled_exact_vs_full_frame(engine, synth, pkg):
 @pytest.mark.parametrize("kw", [dict(), dict(speckle_window_size=30, speckle_range=2), dict(median=1)])
 @pytest.mark.parametrize("f32", [False, True])
 def test_registered_output_copy_out(engine, oracle, synth, pkg, kw, f32):
-    """sgm_host_register'ed outputs (the adapter's persistent disparity_lr): without post
-    filters the WTA runs in row bands whose rows are copied back while the next band is
-    matched; with them, one asynchronous copy after the match. Same result as the oracle and
-    as an unregistered output, in sgm_match (int16) and sgm_match_f32."""
+    """sgm_host_register'ed outputs (the adapter's persistent disparity_lr, copied back by DMA
+    without pageable staging): same result as the oracle and as an unregistered output, with
+    and without post filters, in sgm_match (int16) and sgm_match_f32, the registration reused
+    across calls."""
     h, w, D = 203, 300, 64
     left, right, _ = synth.stereo_pair(h, w, 0, D, seed=77)
     p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, **kw)

@@ -1,7 +1,7 @@
 """A/B of the adapter's copy-out: MatcherCore::forwardMatch (plugin_core_test
 time) on the C3 census frame without post filters, output registered (sgm_host_register) or
-pageable, the registered one copied back in 1 or 4 row bands (SGM_OUT_CHUNKS), interleaved
-rounds. One JSON line per run.
+pageable, interleaved rounds. One JSON line per run. (Round 4 also timed a banded copy-out
+behind a banded WTA, SGM_OUT_CHUNKS=4: no gain, removed; profiles/r04_host_copy_ab.jsonl.)
 
     python tools/host_copy_ab.py [--rounds 3] [--reps 30]
 """
@@ -31,10 +31,8 @@ def main():
         left.tofile(lf)
         right.tofile(rf)
         for rnd in range(a.rounds):
-            for name, reg, chunks in (("pageable", 0, 4), ("registered, 1 copy", 1, 1), ("registered, 4 bands", 1, 4)):
-                env = dict(os.environ, SGM_OUT_CHUNKS=str(chunks))
-                if rnd == 0:
-                    env["SGM_IO_TRACE"] = "1"
+            for name, reg in (("pageable", 0), ("registered", 1)):
+                env = dict(os.environ)
                 r = subprocess.run([core, "time", lf, rf, str(w), str(h), "2", str(D), "0", "5", str(a.reps), "0",
                                     str(reg)], capture_output=True, text=True, timeout=300, env=env)
                 rec = {"round": rnd, "variant": name}
@@ -42,8 +40,6 @@ def main():
                     rec.update(json.loads(r.stdout.strip().splitlines()[-1]))
                 else:
                     rec["error"] = r.stderr[-300:]
-                if rnd == 0:
-                    rec["trace"] = sorted(set(l for l in r.stderr.splitlines() if "[sgm io]" in l))
                 print(json.dumps(rec), flush=True)
 
 
