@@ -472,27 +472,34 @@ template <int R, int DPC, int I>
 __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                                                                  FuseGrid fg, int16_t* __restrict__ C)
 {
+    // every Geom / FuseGrid field the kernel reads, as scalars: a by-value struct that any
+    // lambda captures by reference is otherwise given an address (copied to scratch)
+    const int gW = g.W, gH = g.H, gD = g.D, gP2 = g.P2, gw1 = g.width1, gminD = g.minD, gminX1 = g.minX1;
+    const int gSW2 = g.SW2, gSH2 = g.SH2, gcompat = g.compat, gwide = g.wide, govf_thr = g.ovf_thr;
+    int* const govf = g.ovf;
+    const int fg_strips = fg.strips, fg_chunks = fg.chunks, fg_band_rows = fg.band_rows, fg_ncomp = fg.ncomp;
+    const int fg_total = fg.total, fg_per_xcd = fg.per_xcd, fg_box_segs = fg.box_segs;
     static_assert(DPC / I * kFuseNX == kFuseThreads, "4 threads per staged column");
     static_assert(R <= 21, "ring slots: cases 0..20 below");
     constexpr int TPC = DPC / I;
     extern __shared__ uint32_t lds_fuse[];
     const FuseGeo fz(DPC);
     const int DC = fz.DC, M = fz.M, MH = fz.MH, NX = kFuseNX;
-    const int SW2 = g.SW2, SH2 = g.SH2, XB = NX - 2 * SW2;
+    const int SW2 = gSW2, SH2 = gSH2, XB = NX - 2 * SW2;
     // XCD-aware deal: XCD x = blockIdx.x % 8 runs logical tiles x * per_xcd, x * per_xcd + 1, ...
-    const int lid = (blockIdx.x & 7) * fg.per_xcd + (blockIdx.x >> 3);
-    if (lid >= fg.total) return;
-    const int chunk = lid % fg.chunks, tile = lid / fg.chunks;
-    const int strip = tile % fg.strips, band = tile / fg.strips;
+    const int lid = (blockIdx.x & 7) * fg_per_xcd + (blockIdx.x >> 3);
+    if (lid >= fg_total) return;
+    const int chunk = lid % fg_chunks, tile = lid / fg_chunks;
+    const int strip = tile % fg_strips, band = tile / fg_strips;
     const int x0 = strip * XB, d0 = chunk * DC;
-    const int y0 = band * fg.band_rows, y1 = min(fg.ncomp, y0 + fg.band_rows);
+    const int y0 = band * fg_band_rows, y1 = min(fg_ncomp, y0 + fg_band_rows);
     const int nv = (y1 - y0) + 2 * SH2;                      // rows of P the band needs
     const int t = threadIdx.x;
     uint32_t* S0 = lds_fuse;                                 // staging, two buffers
     uint32_t* V0 = lds_fuse + 2 * fz.stage_words();          // V rows [NX][DPC], two buffers
-    const int xs = g.minX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
-    const int xr0 = xs - g.minD - (d0 + DC - 1);             // right entry r <-> xr0 + r
-    const size_t plane = (size_t)g.W * g.H;
+    const int xs = gminX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
+    const int xr0 = xs - gminD - (d0 + DC - 1);             // right entry r <-> xr0 + r
+    const size_t plane = (size_t)gW * gH;
     // staging (waves 4-7, beside the box of waves 0-3): entry st of the 2 * NX left entries (one
     // each) and entries st, st + 256 of the 2 * NRr right ones; the bt words of row v + 2 are
     // loaded while row v + 1's are written to LDS, so a global load's latency spans a whole phase
@@ -502,12 +509,12 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int cr0 = st >= NRr, r0 = st - cr0 * NRr;
     const bool has1 = st + 256 < 2 * NRr;
     const int cr1 = st + 256 >= NRr, r1 = st + 256 - cr1 * NRr;
-    const uint32_t* btL = bt + cl * plane + min(max(xs + kl, 0), g.W - 1);
-    const uint32_t* btR0 = bt + (2 + cr0) * plane + min(max(xr0 + r0, 0), g.W - 1);
-    const uint32_t* btR1 = bt + (2 + cr1) * plane + min(max(xr0 + r1, 0), g.W - 1);
+    const uint32_t* btL = bt + cl * plane + min(max(xs + kl, 0), gW - 1);
+    const uint32_t* btR0 = bt + (2 + cr0) * plane + min(max(xr0 + r0, 0), gW - 1);
+    const uint32_t* btR1 = bt + (2 + cr1) * plane + min(max(xr0 + r1, 0), gW - 1);
     uint32_t wl = 0, wr0 = 0, wr1 = 0;
     auto stage_load = [&](int v) {
-        const size_t ro = (size_t)min(max(y0 - SH2 + v, 0), g.H - 1) * g.W;
+        const size_t ro = (size_t)min(max(y0 - SH2 + v, 0), gH - 1) * gW;
         wl = btL[ro];
         wr0 = btR0[ro];
         wr1 = has1 ? btR1[ro] : 0u;
@@ -542,19 +549,19 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
     // box: thread (segment, pair) of waves 0-3
-    const int nout = min(XB, g.width1 - x0);
-    const int klo = max(SW2 - x0, 0), khi = min(g.width1 - 1 - x0 + SW2, NX - 1);
+    const int nout = min(XB, gw1 - x0);
+    const int klo = max(SW2 - x0, 0), khi = min(gw1 - 1 - x0 + SW2, NX - 1);
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
-    const int NSEG = fg.box_segs;                            // <= 256 / DPC
+    const int NSEG = fg_box_segs;                            // <= 256 / DPC
     const int bp = t % DPC, bseg = t / DPC;
     const int seglen = (nout + NSEG - 1) / NSEG;
     const int xa = bseg < NSEG ? bseg * seglen : nout, xb = min(xa + seglen, nout);
     u16x2_t bmax = {0, 0};                                   // flag: the largest box sum seen
-    const bool col0 = (g.compat & SGM_OCV_COL0_LEGACY) && x0 == 0;
-    const u16x2_t p2v = {(unsigned short)g.P2, (unsigned short)g.P2};
+    const bool col0 = (gcompat & SGM_OCV_COL0_LEGACY) && x0 == 0;
+    const u16x2_t p2v = {(unsigned short)gP2, (unsigned short)gP2};
     uint32_t* C32 = (uint32_t*)C;
-    const size_t rowC = (size_t)g.width1 * g.D / 2;         // u32 per C' row
-    const bool last_band = y1 == fg.ncomp;
+    const size_t rowC = (size_t)gw1 * gD / 2;         // u32 per C' row
+    const bool last_band = y1 == fg_ncomp;
     if (t >= 256) {
         stage_load(0);
         stage_store(S0);
@@ -611,24 +618,24 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
         }
         if (t < 256 && v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {   // the box of row v - 1
             const int y = y0 + (v - 1) - 2 * SH2;
-            const bool tail = last_band && y == fg.ncomp - 1;
+            const bool tail = last_band && y == fg_ncomp - 1;
             const uint32_t* Vp = V0 + ((v - 1) & 1) * NX * DPC + bp;
-            auto slide = [&](auto clampit) {
-                auto rd = [&](int k) {
+            auto slide = [&](auto clampit) __attribute__((always_inline)) {
+                auto rd = [&](int k) __attribute__((always_inline)) {
                     if constexpr (decltype(clampit)::value) k = min(max(k, klo), khi);
                     return __builtin_bit_cast(u16x2_t, Vp[k * DPC]);
                 };
                 u16x2_t sum = {0, 0};
                 for (int u2 = 0; u2 <= 2 * SW2; u2++) sum += rd(xa + u2);
-                uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * g.D + d0) / 2 + bp;
+                uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * gD + d0) / 2 + bp;
                 for (int xo = xa; xo < xb; xo++) {
                     if (xo > xa) sum += rd(xo + 2 * SW2) - rd(xo - 1);
                     if (!(col0 && xo == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
                     const uint32_t c = __builtin_bit_cast(uint32_t, sum + p2v);
                     o[0] = c;
                     if (tail)                                // OpenCV's bottom rows: never recomputed
-                        for (int yy = y + 1; yy < g.H; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? g.P2 * 0x10001u : c;
-                    o += g.D / 2;
+                        for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? gP2 * 0x10001u : c;
+                    o += gD / 2;
                 }
             };
             if (edge) slide(std::true_type{});
@@ -640,11 +647,11 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
         }
         __syncthreads();
     }
-    if (g.wide == 2 && g.ovf && t < 256) {
+    if (gwide == 2 && govf && t < 256) {
         const int m = max((int)bmax[0], (int)bmax[1]);
-        const bool ovf = m > g.ovf_thr - g.P2;
+        const bool ovf = m > govf_thr - gP2;
         const uint64_t b = __ballot(ovf);
-        if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(g.ovf, 1);
+        if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(govf, 1);
     }
 }
 
