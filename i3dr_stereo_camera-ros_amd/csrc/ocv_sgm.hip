@@ -670,9 +670,10 @@ __host__ inline bool ocv_cost_fusable(const Geom& g)
 {
     const long long B = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63);
     const char* e = std::getenv("SGM_OCV_FUSED");
-    // default: frames with enough tiles x bands to fill the chip, and boxes up to 9 x 9 (wider
-    // ones need long horizontal windows that the two-kernel form slides more cheaply: the
-    // shipped block-21 config measured 5.2 fused vs 3.8 ms, profiles/r04_ocv_cost_ab.jsonl)
+    // default: frames with enough tiles x bands to fill the chip (10^8 cells: C1 measured 0.12-0.15
+    // fused vs 0.053 ms), and boxes up to 9 x 9 (wider ones need 2*SW2+1-column horizontal windows
+    // over short per-thread segments and 2*SH2+1-slot register rings, one block per CU: the
+    // shipped block-21 config measured 4.8-5.1 fused vs 3.8 ms; profiles/r04_ocv_cost_ab.jsonl)
     const bool dflt = (double)g.width1 * g.H * g.D >= 1e8 && g.SH2 <= 4;
     return g.SH2 <= 10 && g.SW2 <= 10 && B <= 65535 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
 }
@@ -1502,7 +1503,7 @@ static FuseGrid fuse_grid(const Geom& g)
     const long long tiles = (long long)fg.strips * fg.chunks;
     const char* e = std::getenv("SGM_FUSE_ROWS");
     fg.band_rows = e ? std::max(std::atoi(e), 1)
-                     : (int)std::max<long long>(std::max(16, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
+                     : (int)std::max<long long>(std::max(64, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;
