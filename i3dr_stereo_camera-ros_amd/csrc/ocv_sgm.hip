@@ -46,9 +46,13 @@ constexpr int kMaxCost = 32767;
                            // 1 step 1.42 ms, 2 steps 0.95, 3 steps 1.57, 4 steps 1.25)
 #endif
 
+// bt (optional, the fused cost's input): the Birchfield-Tomasi intervals of both channels at x,
+// packed u | lo << 8 | hi << 16, from the prefiltered / raw values at x - 1, x, x + 1 computed in
+// the thread (what bt_lohi reads from the planes)
 __global__ __launch_bounds__(256) void k_ocv_prefilter(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                        size_t stride, int W, int H, int ftzero,
-                                                       uint8_t* __restrict__ planes /* 4 x W x H */)
+                                                       uint8_t* __restrict__ planes /* 4 x W x H */,
+                                                       uint32_t* __restrict__ bt /* 4 x W x H, or null */)
 {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
@@ -57,13 +61,30 @@ __global__ __launch_bounds__(256) void k_ocv_prefilter(const uint8_t* __restrict
     uint8_t* pf = planes + (size_t)(2 * img) * W * H;
     uint8_t* raw = planes + (size_t)(2 * img + 1) * W * H;
     const size_t o = (size_t)y * W + x;
-    if (x == 0 || x == W - 1) { pf[o] = (uint8_t)ftzero; raw[o] = (uint8_t)ftzero; return; }
     const uint8_t* r = src + (size_t)y * stride;
     const uint8_t* n = y > 0 ? r - stride : r;
     const uint8_t* s = y < H - 1 ? r + stride : r;
-    const int v = (r[x + 1] - r[x - 1]) * 2 + n[x + 1] - n[x - 1] + s[x + 1] - s[x - 1];
-    pf[o] = (uint8_t)(min(max(v, -ftzero), ftzero) + ftzero);
-    raw[o] = r[x];
+    auto pfraw = [&](int xx, int& p, int& q) {           // columns 0 and W - 1 are ftzero
+        if (xx <= 0 || xx >= W - 1) { p = ftzero; q = ftzero; return; }
+        const int v = (r[xx + 1] - r[xx - 1]) * 2 + n[xx + 1] - n[xx - 1] + s[xx + 1] - s[xx - 1];
+        p = min(max(v, -ftzero), ftzero) + ftzero;
+        q = r[xx];
+    };
+    int p0, q0;
+    pfraw(x, p0, q0);
+    pf[o] = (uint8_t)p0;
+    raw[o] = (uint8_t)q0;
+    if (!bt) return;
+    int pl = p0, ql = q0, pr = p0, qr = q0;
+    if (x > 0) pfraw(x - 1, pl, ql);
+    if (x < W - 1) pfraw(x + 1, pr, qr);
+    auto pack = [](int u, int a, int b) {                 // bt_lohi with neighbours a (x - 1), b (x + 1)
+        const int ul = (u + a) / 2, ur = (u + b) / 2;
+        return (uint32_t)u | (uint32_t)min(min(ul, ur), u) << 8 | (uint32_t)max(max(ul, ur), u) << 16;
+    };
+    const size_t plane = (size_t)W * H;
+    bt[(size_t)(2 * img) * plane + o] = pack(p0, pl, pr);
+    bt[(size_t)(2 * img + 1) * plane + o] = pack(q0, ql, qr);
 }
 
 __device__ __forceinline__ void bt_lohi(const uint8_t* a, int x, int W, int& u, int& lo, int& hi)
@@ -412,26 +433,13 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_sat(const int16_t* __restrict_
     }
 }
 
-// Birchfield-Tomasi intervals of the four planes (left pf, left raw, right pf, right raw),
-// packed u | lo << 8 | hi << 16 per pixel: what every fused-cost block stages per row (one
-// dword load per entry instead of three byte loads and the min/max).
-__global__ __launch_bounds__(256) void k_ocv_btplanes(const uint8_t* __restrict__ planes, int W, int H,
-                                                      uint32_t* __restrict__ bt)
-{
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
-    if (x >= W) return;
-    int u, lo, hi;
-    bt_lohi(planes + (size_t)c * W * H + (size_t)y * W, x, W, u, lo, hi);
-    bt[((size_t)c * H + y) * W + x] = (uint32_t)u | (uint32_t)lo << 8 | (uint32_t)hi << 16;
-}
-
 // ---- the whole cost stage in one pass: pixel cost + vertical box + horizontal box + P2 ------
 // (replaces k_ocv_pixhsum + k_ocv_vsum_seg, whose 2 B/cell horizontal-sum volume went to HBM
 // and was read back twice: 1.71 GB moved for 0.50 GB of C' at 1080p D=128, PMC r03). The box
 // is separable and OpenCV's int16 wrap is arithmetic mod 2^16, so the vertical sums can come
 // first: a block owns a tile of XB output columns x DC disparities over a band of rows and walks
 // the band's rows (+ SH2 above and below) once. Per row:
-//   staging threads (waves 4-7): the BT intervals of the row (k_ocv_btplanes) into LDS in
+//   staging threads (waves 4-7): the BT intervals of the row (k_ocv_prefilter writes them) into LDS in
 //       k_ocv_pixhsum's formats (left columns duplicated into both halves of a word, right
 //       entries as pair words of adjacent disparities);
 //   every thread: the pixel costs of its staged column k and I disparity pairs (packed u16 ops,
@@ -659,9 +667,12 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
 // single C row is never updated there) or the P2 initialisation (MODE_HH)
 __global__ __launch_bounds__(256) void k_ocv_col0_legacy(Geom g, int fullDP, int16_t* __restrict__ C)
 {
-    const int d = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y + 1;
-    if (d >= g.D) return;
-    C[(size_t)y * g.width1 * g.D + d] = fullDP ? (int16_t)g.P2 : C[d];
+    const int np = g.D / 2;                               // u32 pairs of column 0
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (g.H - 1) * np) return;
+    const int y = 1 + i / np, pr = i - (y - 1) * np;
+    uint32_t* C32 = (uint32_t*)C;
+    C32[(size_t)y * g.width1 * np + pr] = fullDP ? ((uint32_t)g.P2 & 0xFFFFu) * 0x10001u : C32[pr];
 }
 
 // The fused cost applies: R = 2*SH2 + 1 <= 21 (the register ring; SH2 <= 10 leaves XB >= 108 of
@@ -1515,7 +1526,7 @@ static FuseGrid fuse_grid(const Geom& g)
 }
 
 // C' of the frame into bufA (bufB: scratch, the horizontal sums of the unfused kernels).
-// Default: k_ocv_btplanes + k_ocv_cost_fused (+ k_ocv_col0_legacy) when ocv_cost_fusable, else
+// Default: k_ocv_prefilter (with the BT planes) + k_ocv_cost_fused (+ k_ocv_col0_legacy) when ocv_cost_fusable, else
 // k_ocv_pixhsum (or k_ocv_pixcost + k_ocv_hsum) + k_ocv_vsum_seg. SIMD_SAT frames that take the
 // flagged kernels (Geom::wide != 0 and the overflow flag) get the exact SIMD cost written over
 // it, by kernels that return at once on the other frames: the vertical SIMD update over the
@@ -1525,15 +1536,14 @@ static FuseGrid fuse_grid(const Geom& g)
 hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, const Geom& g, int fullDP,
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
-                       g.ftzero, planes);
     const size_t lds = pix_lds_bytes(g);
     const bool fused = ocv_cost_fusable(g);
+    uint32_t* bt = fused ? (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H)) : nullptr;
+    hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
+                       g.ftzero, planes, bt);
     const bool sat2 = g.wide && (g.compat & SGM_OCV_SIMD_SAT) && ocv_hsum_cannot_saturate(g) &&
                       (size_t)(2 * g.SH2 + 1) * 256 * 4 <= 64 * 1024 && !std::getenv("SGM_OCV_SAT_SEQ");
     if (fused) {
-        uint32_t* bt = (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H));
-        hipLaunchKernelGGL(k_ocv_btplanes, dim3((g.W + 255) / 256, g.H, 4), dim3(256), 0, st, planes, g.W, g.H, bt);
         const FuseGrid fg = fuse_grid(g);
         switch (g.SH2) {
         case 0: launch_cost_fused_r<1>(bt, g, fullDP, fg, bufA, st); break;
@@ -1549,7 +1559,8 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
         default: launch_cost_fused_r<21>(bt, g, fullDP, fg, bufA, st); break;
         }
         if ((g.compat & SGM_OCV_COL0_LEGACY) && g.H > 1)
-            hipLaunchKernelGGL(k_ocv_col0_legacy, dim3((g.D + 255) / 256, g.H - 1), dim3(256), 0, st, g, fullDP, bufA);
+            hipLaunchKernelGGL(k_ocv_col0_legacy, dim3(((g.H - 1) * (g.D / 2) + 255) / 256), dim3(256), 0, st, g, fullDP,
+                               bufA);
         if (sat2) {                    // the flagged frames' horizontal sums for k_ocv_vsum_sat2
             const int XB = pix_xb(g), DC = pix_dc(g);
             hipLaunchKernelGGL(k_ocv_pixhsum<true>, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256),
