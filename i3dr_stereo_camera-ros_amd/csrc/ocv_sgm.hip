@@ -475,6 +475,7 @@ struct FuseGeo {
 struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
     int box_segs;            // output segments per disparity pair (the box threads: box_segs * DPC)
+    int box_threads;         // 256 (waves 0-3, beside the staging waves) or 512 (every wave)
 };
 template <int R, int DPC, int I>
 __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int gSW2 = g.SW2, gSH2 = g.SH2, gcompat = g.compat, gwide = g.wide, govf_thr = g.ovf_thr;
     int* const govf = g.ovf;
     const int fg_strips = fg.strips, fg_chunks = fg.chunks, fg_band_rows = fg.band_rows, fg_ncomp = fg.ncomp;
-    const int fg_total = fg.total, fg_per_xcd = fg.per_xcd, fg_box_segs = fg.box_segs;
+    const int fg_total = fg.total, fg_per_xcd = fg.per_xcd, fg_box_segs = fg.box_segs, nbox = fg.box_threads;
     static_assert(DPC / I * kFuseNX == kFuseThreads, "4 threads per staged column");
     static_assert(R <= 21, "ring slots: cases 0..20 below");
     constexpr int TPC = DPC / I;
@@ -560,7 +561,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int nout = min(XB, gw1 - x0);
     const int klo = max(SW2 - x0, 0), khi = min(gw1 - 1 - x0 + SW2, NX - 1);
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
-    const int NSEG = fg_box_segs;                            // <= 256 / DPC
+    const int NSEG = fg_box_segs;                            // <= nbox / DPC
     const int bp = t % DPC, bseg = t / DPC;
     const int seglen = (nout + NSEG - 1) / NSEG;
     const int xa = bseg < NSEG ? bseg * seglen : nout, xb = min(xa + seglen, nout);
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
                 for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
             }
         }
-        if (t < 256 && v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {   // the box of row v - 1
+        if (t < nbox && v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {   // the box of row v - 1
             const int y = y0 + (v - 1) - 2 * SH2;
             const bool tail = last_band && y == fg_ncomp - 1;
             const uint32_t* Vp = V0 + ((v - 1) & 1) * NX * DPC + bp;
@@ -655,7 +656,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
         }
         __syncthreads();
     }
-    if (gwide == 2 && govf && t < 256) {
+    if (gwide == 2 && govf && t < nbox) {
         const int m = max((int)bmax[0], (int)bmax[1]);
         const bool ovf = m > govf_thr - gP2;
         const uint64_t b = __ballot(ovf);
@@ -1520,8 +1521,11 @@ static FuseGrid fuse_grid(const Geom& g)
     fg.per_xcd = (fg.total + 7) / 8;
     // box segments per pair: every thread by default (each slides its window over
     // seglen = XB / segs outputs after a 2*SW2+1 read start); SGM_FUSE_BOXSEG for fewer, longer ones
-    fg.box_segs = 256 / dpc;
-    if (const char* b = std::getenv("SGM_FUSE_BOXSEG")) fg.box_segs = std::min(std::max(std::atoi(b), 1), 256 / dpc);
+    const char* ba = std::getenv("SGM_FUSE_BOXALL");
+    fg.box_threads = ba && std::atoi(ba) ? kFuseThreads : 256;
+    fg.box_segs = fg.box_threads / dpc;
+    if (const char* b = std::getenv("SGM_FUSE_BOXSEG"))
+        fg.box_segs = std::min(std::max(std::atoi(b), 1), fg.box_threads / dpc);
     return fg;
 }
 
