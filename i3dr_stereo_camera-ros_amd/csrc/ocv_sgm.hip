@@ -444,11 +444,13 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_sat(const int16_t* __restrict_
 //       entries as pair words of adjacent disparities);
 //   every thread: the pixel costs of its staged column k and I disparity pairs (packed u16 ops,
 //       the left words kept in registers), and its vertical window sums V: V += P - P(row - R),
-//       the last R = 2*SH2 + 1 rows of P in registers (the row loop is unrolled by R, so every
-//       ring slot is a static register); V of the row to LDS;
-//   box threads (waves 0-3): the horizontal box of the previous row's V (a sliding window per
-//       segment of output columns, staged columns outside [0, width1) read as the edge column:
-//       OpenCV's replicate rule), + P2, stored as int16 (u16 wrap = OpenCV's CostType store);
+//       the last R = 2*SH2 + 1 rows of P in registers (the slot is picked by a uniform switch,
+//       so every ring slot is a static register); V of the row to LDS;
+//   box threads (every wave for R <= 9, else waves 0-3): the horizontal box (2*SW2+1 = R wide:
+//       OpenCV's block is square) of the previous row's V: a segment of L output columns per
+//       thread and pair, its L + R - 1 window values read from LDS at once (staged columns
+//       outside [0, width1) read as the edge column: OpenCV's replicate rule) and slid over in
+//       registers, + P2, stored as int16 (u16 wrap = OpenCV's CostType store);
 // one barrier per row (staging, V and the box double-buffered). The true sums are exact in u16
 // when (2*SW2+1)(2*SH2+1)(2*ftzero+63) <= 65535 (the launcher's condition), so the overflow flag
 // of Geom::wide == 2 is max(box) > ovf_thr - P2, as k_ocv_vsum_seg computes it (no horizontal sum
@@ -474,11 +476,19 @@ struct FuseGeo {
 };
 struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
-    int box_segs;            // output segments per disparity pair (the box threads: box_segs * DPC)
-    int box_threads;         // 256 (waves 0-3, beside the staging waves) or 512 (every wave)
 };
 template <int R, int DPC, int I>
-__global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
+#ifndef SGM_FUSE_BOX_EARLY
+#define SGM_FUSE_BOX_EARLY 1     // A/B: the box reads issued before the pixel costs (0: after the V store)
+#endif
+#ifndef SGM_FUSE_NB_WIDE
+#define SGM_FUSE_NB_WIDE 256     // A/B: box threads for R > 9 (512: every wave)
+#endif
+#ifndef SGM_FUSE_WPE5
+#define SGM_FUSE_WPE5 1          // A/B: waves per SIMD asked of the R <= 5, 32-pair build (4: <= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(kFuseThreads) __attribute__((amdgpu_waves_per_eu((R <= 5 && DPC == 32) ? SGM_FUSE_WPE5 : 1)))
+void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                                                                  FuseGrid fg, int16_t* __restrict__ C)
 {
     // every Geom / FuseGrid field the kernel reads, as scalars: a by-value struct that any
@@ -487,7 +497,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     const int gSW2 = g.SW2, gSH2 = g.SH2, gcompat = g.compat, gwide = g.wide, govf_thr = g.ovf_thr;
     int* const govf = g.ovf;
     const int fg_strips = fg.strips, fg_chunks = fg.chunks, fg_band_rows = fg.band_rows, fg_ncomp = fg.ncomp;
-    const int fg_total = fg.total, fg_per_xcd = fg.per_xcd, fg_box_segs = fg.box_segs, nbox = fg.box_threads;
+    const int fg_total = fg.total, fg_per_xcd = fg.per_xcd;
     static_assert(DPC / I * kFuseNX == kFuseThreads, "4 threads per staged column");
     static_assert(R <= 21, "ring slots: cases 0..20 below");
     constexpr int TPC = DPC / I;
@@ -557,29 +567,54 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
     }
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
-    // box: thread (segment, pair) of waves 0-3
+    // box: thread (segment, pair); NB box threads, L outputs per segment, the NL = L + R - 1
+    // window values of a segment read from LDS at once (one wait, not one per output)
+    constexpr int NB = R <= 9 ? kFuseThreads : SGM_FUSE_NB_WIDE;   // every wave for small boxes, else waves 0-3
+    constexpr int NSEG = NB / DPC;
+    constexpr int L = (kFuseNX - (R - 1) + NSEG - 1) / NSEG;
+    constexpr int NL = L + R - 1;
     const int nout = min(XB, gw1 - x0);
     const int klo = max(SW2 - x0, 0), khi = min(gw1 - 1 - x0 + SW2, NX - 1);
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
-    const int NSEG = fg_box_segs;                            // <= nbox / DPC
     const int bp = t % DPC, bseg = t / DPC;
-    const int seglen = (nout + NSEG - 1) / NSEG;
-    const int xa = bseg < NSEG ? bseg * seglen : nout, xb = min(xa + seglen, nout);
+    const int xa = bseg * L, xb = min(xa + L, nout);
     u16x2_t bmax = {0, 0};                                   // flag: the largest box sum seen
     const bool col0 = (gcompat & SGM_OCV_COL0_LEGACY) && x0 == 0;
     const u16x2_t p2v = {(unsigned short)gP2, (unsigned short)gP2};
     uint32_t* C32 = (uint32_t*)C;
     const size_t rowC = (size_t)gw1 * gD / 2;         // u32 per C' row
     const bool last_band = y1 == fg_ncomp;
+    int v_cur = 0;                                           // the row of the loop below
     if (t >= 256) {
         stage_load(0);
         stage_store(S0);
         if (1 < nv) stage_load(1);
     }
     __syncthreads();
+    auto box_load = [&](u16x2_t (&w)[NL]) __attribute__((always_inline)) {
+        const uint32_t* Vp = V0 + ((v_cur - 1) & 1) * NX * DPC + bp;
+        if (edge) {                                          // staged columns outside the frame: the edge column
+#pragma unroll
+            for (int i = 0; i < NL; i++) w[i] = wd(Vp, min(max(xa + i, klo), khi) * DPC);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NL; i++) {
+                // only the last segment's window passes the staged row (L * NSEG >= XB)
+                const int k = i > NX - 1 - (NSEG - 1) * L ? min(xa + i, NX - 1) : xa + i;
+                w[i] = wd(Vp, k * DPC);
+            }
+        }
+    };
     int slot = 0;
     for (int v = 0; v <= nv; v++) {
+        v_cur = v;
         uint32_t* S = S0 + (v & 1) * fz.stage_words();
+        // the box's window values of row v - 1 are read before the pixel costs of row v are
+        // computed (independent LDS buffers), so their latency hides behind that work
+        const bool dobox = t < NB && v >= 1 && v - 1 >= 2 * SH2 && xa < xb;
+        u16x2_t w[NL];
+        if constexpr (SGM_FUSE_BOX_EARLY)
+            if (dobox) box_load(w);
         if (v < nv) {
             const uint32_t* Lk = S + 6 * kc;
             u16x2_t u[2], ulo[2], uhi[2];
@@ -625,30 +660,31 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
                 for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
             }
         }
-        if (t < nbox && v >= 1 && v - 1 >= 2 * SH2 && xa < xb) {   // the box of row v - 1
+        if (dobox) {                                         // the box of row v - 1
             const int y = y0 + (v - 1) - 2 * SH2;
             const bool tail = last_band && y == fg_ncomp - 1;
-            const uint32_t* Vp = V0 + ((v - 1) & 1) * NX * DPC + bp;
-            auto slide = [&](auto clampit) __attribute__((always_inline)) {
-                auto rd = [&](int k) __attribute__((always_inline)) {
-                    if constexpr (decltype(clampit)::value) k = min(max(k, klo), khi);
-                    return __builtin_bit_cast(u16x2_t, Vp[k * DPC]);
-                };
-                u16x2_t sum = {0, 0};
-                for (int u2 = 0; u2 <= 2 * SW2; u2++) sum += rd(xa + u2);
-                uint32_t* o = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * gD + d0) / 2 + bp;
-                for (int xo = xa; xo < xb; xo++) {
-                    if (xo > xa) sum += rd(xo + 2 * SW2) - rd(xo - 1);
-                    if (!(col0 && xo == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
-                    const uint32_t c = __builtin_bit_cast(uint32_t, sum + p2v);
-                    o[0] = c;
-                    if (tail)                                // OpenCV's bottom rows: never recomputed
-                        for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = fullDP ? gP2 * 0x10001u : c;
-                    o += gD / 2;
+            if constexpr (!SGM_FUSE_BOX_EARLY) box_load(w);
+            u16x2_t sum = w[0];
+#pragma unroll
+            for (int i = 1; i < R; i++) sum += w[i];
+            uint32_t* const o0 = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * gD + d0) / 2 + bp;
+            uint32_t* o = o0;
+#pragma unroll
+            for (int j = 0; j < L; j++) {
+                if (j > 0) sum += w[j + R - 1] - w[j - 1];
+                if (xa + j < xb) {
+                    if (!(col0 && xa + j == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
+                    o[0] = __builtin_bit_cast(uint32_t, sum + p2v);
                 }
-            };
-            if (edge) slide(std::true_type{});
-            else slide(std::false_type{});
+                o += gD / 2;
+            }
+            if (tail) {                                      // OpenCV's bottom rows: never recomputed
+                o = o0;
+                for (int xo = xa; xo < xb; xo++, o += gD / 2) {
+                    const uint32_t c = fullDP ? gP2 * 0x10001u : o[0];   // this thread's own store
+                    for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
+                }
+            }
         }
         if (t >= 256 && v + 1 < nv) {
             stage_store(S0 + ((v + 1) & 1) * fz.stage_words());
@@ -656,7 +692,7 @@ __global__ __launch_bounds__(kFuseThreads) void k_ocv_cost_fused(const uint32_t*
         }
         __syncthreads();
     }
-    if (gwide == 2 && govf && t < nbox) {
+    if (gwide == 2 && govf && t < NB) {
         const int m = max((int)bmax[0], (int)bmax[1]);
         const bool ovf = m > govf_thr - gP2;
         const uint64_t b = __ballot(ovf);
@@ -682,12 +718,11 @@ __host__ inline bool ocv_cost_fusable(const Geom& g)
 {
     const long long B = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63);
     const char* e = std::getenv("SGM_OCV_FUSED");
-    // default: frames with enough tiles x bands to fill the chip (10^8 cells: C1 measured 0.12-0.15
-    // fused vs 0.053 ms), and boxes up to 9 x 9 (wider ones need 2*SW2+1-column horizontal windows
-    // over short per-thread segments and 2*SH2+1-slot register rings, one block per CU: the
-    // shipped block-21 config measured 4.8-5.1 fused vs 3.8 ms; profiles/r04_ocv_cost_ab.jsonl)
-    const bool dflt = (double)g.width1 * g.H * g.D >= 1e8 && g.SH2 <= 4;
-    return g.SH2 <= 10 && g.SW2 <= 10 && B <= 65535 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
+    // default: frames with enough tiles x bands to fill the chip (10^8 cells: C1 measured 0.10
+    // fused vs 0.053 ms; 1080p block 5 0.29 vs 0.42, the shipped block-21 config 3.18 vs 3.79 ms,
+    // profiles/r04_ocv_cost_box_ab.jsonl)
+    const bool dflt = (double)g.width1 * g.H * g.D >= 1e8;
+    return g.SH2 <= 10 && g.SW2 == g.SH2 && B <= 65535 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
 }
 
 // The SIMD_SAT flagged frames whose horizontal sums cannot saturate: when
@@ -1433,11 +1468,16 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
         // every S saturated at MAX_COST: bestDisp stays -1 in OpenCV (see k_ocv_wta16)
         const bool rej = __ballot(hit) != 0ull || minS >= 32767;
         auto s_at = [&](int d) {                       // S[d] of the pixel (d wave-uniform)
-            const int kk = d % DPL;
-            int v = S[0];
+            // one readlane per element, the element picked among the scalars: a select over the
+            // S registers themselves is folded into an indexed load, which puts S in LDS
+            const int kk = d % DPL, ln = d / DPL;
+            int v = __builtin_amdgcn_readlane(S[0], ln);
 #pragma unroll
-            for (int k = 1; k < DPL; k++) v = kk == k ? S[k] : v;
-            return __builtin_amdgcn_readlane(v, d / DPL);
+            for (int k = 1; k < DPL; k++) {
+                const int r = __builtin_amdgcn_readlane(S[k], ln);
+                v = kk == k ? r : v;
+            }
+            return v;
         };
         const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, g.D - 1));
         const int den = max(sm + sp - 2 * minS, 1);
@@ -1519,13 +1559,6 @@ static FuseGrid fuse_grid(const Geom& g)
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;
-    // box segments per pair: every thread by default (each slides its window over
-    // seglen = XB / segs outputs after a 2*SW2+1 read start); SGM_FUSE_BOXSEG for fewer, longer ones
-    const char* ba = std::getenv("SGM_FUSE_BOXALL");
-    fg.box_threads = ba && std::atoi(ba) ? kFuseThreads : 256;
-    fg.box_segs = fg.box_threads / dpc;
-    if (const char* b = std::getenv("SGM_FUSE_BOXSEG"))
-        fg.box_segs = std::min(std::max(std::atoi(b), 1), fg.box_threads / dpc);
     return fg;
 }
 
@@ -1541,13 +1574,21 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
 {
     const size_t lds = pix_lds_bytes(g);
-    const bool fused = ocv_cost_fusable(g);
+    // wide == 1 with SIMD_SAT: every launch after this one reads the SIMD cost, the plain C' is never used
+    const bool simd_only = g.wide == 1 && (g.compat & SGM_OCV_SIMD_SAT);
+    const bool fused = !simd_only && ocv_cost_fusable(g);
     uint32_t* bt = fused ? (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H)) : nullptr;
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes, bt);
-    const bool sat2 = g.wide && (g.compat & SGM_OCV_SIMD_SAT) && ocv_hsum_cannot_saturate(g) &&
+    const bool sat2 = g.wide && (g.compat & SGM_OCV_SIMD_SAT) && ocv_hsum_cannot_saturate(g) && lds <= 64 * 1024 &&
                       (size_t)(2 * g.SH2 + 1) * 256 * 4 <= 64 * 1024 && !std::getenv("SGM_OCV_SAT_SEQ");
-    if (fused) {
+    if (simd_only) {
+        if (sat2) {                    // the horizontal sums for k_ocv_vsum_sat2
+            const int XB = pix_xb(g), DC = pix_dc(g);
+            hipLaunchKernelGGL(k_ocv_pixhsum<true>, dim3((g.width1 + XB - 1) / XB, g.H, (g.D + DC - 1) / DC), dim3(256),
+                               lds, st, planes, g, bufB);
+        }
+    } else if (fused) {
         const FuseGrid fg = fuse_grid(g);
         switch (g.SH2) {
         case 0: launch_cost_fused_r<1>(bt, g, fullDP, fg, bufA, st); break;

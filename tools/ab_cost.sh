@@ -16,6 +16,7 @@ for r in $(seq "$rounds"); do
       fused8) env=(SGM_OCV_FUSED=1 SGM_FUSE_DPC=8) ;;
       fused_seg*) env=(SGM_OCV_FUSED=1 SGM_FUSE_BOXSEG=${v#fused_seg}) ;;
       fused_boxall) env=(SGM_OCV_FUSED=1 SGM_FUSE_BOXALL=1) ;;
+      fused_box4) env=(SGM_OCV_FUSED=1 SGM_FUSE_BOXALL=0) ;;
       fused_rows*) env=(SGM_OCV_FUSED=1 SGM_FUSE_ROWS=${v#fused_rows}) ;;
     esac
     env "${env[@]}" timeout -k 10 300 python tools/ocv_modes_bench.py --reps 5 --case "$case" > gpurun_out/ab_cost_one.log 2>&1 || exit 1
