@@ -478,16 +478,23 @@ struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
 };
 template <int R, int DPC, int I>
+// A/B knobs of k_ocv_cost_fused (-1: the measured default, by box size R; profiles/r04_ocv_cost_ring_ab.jsonl:
+// R <= 9 (1080p block 5) 0.302 -> 0.239 ms with both on, two blocks per CU at 113 VGPRs; R = 21 (the shipped
+// block 21) 3.18 ms with both off against 3.61 (ring bytes) / 4.58 (early box reads): one block per CU either
+// way, where the extra registers and repacking only add work)
+#ifndef SGM_FUSE_RING8
+#define SGM_FUSE_RING8 -1        // the pixel-cost ring as bytes (half the registers)
+#endif
 #ifndef SGM_FUSE_BOX_EARLY
-#define SGM_FUSE_BOX_EARLY 1     // A/B: the box reads issued before the pixel costs (0: after the V store)
+#define SGM_FUSE_BOX_EARLY -1    // the box reads issued before the pixel costs (else after the V store)
 #endif
 #ifndef SGM_FUSE_NB_WIDE
 #define SGM_FUSE_NB_WIDE 256     // A/B: box threads for R > 9 (512: every wave)
 #endif
-#ifndef SGM_FUSE_WPE5
-#define SGM_FUSE_WPE5 1          // A/B: waves per SIMD asked of the R <= 5, 32-pair build (4: <= 128 VGPRs)
+#ifndef SGM_FUSE_WPE
+#define SGM_FUSE_WPE 1           // A/B: waves per SIMD asked of the compiler (4: <= 128 VGPRs, two blocks per CU)
 #endif
-__global__ __launch_bounds__(kFuseThreads) __attribute__((amdgpu_waves_per_eu((R <= 5 && DPC == 32) ? SGM_FUSE_WPE5 : 1)))
+__global__ __launch_bounds__(kFuseThreads) __attribute__((amdgpu_waves_per_eu(SGM_FUSE_WPE)))
 void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                                                                  FuseGrid fg, int16_t* __restrict__ C)
 {
@@ -557,14 +564,19 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     // registers, slot v mod R picked by a uniform switch (static register indices, one copy of
     // the row code)
     const int kc = t / TPC, tq = t % TPC;
-    uint32_t ring[I][R];
+    // kRing8: a pixel cost is <= 2*ftzero + 63 <= 255 (the launcher's condition), so the ring
+    // keeps bytes, two disparity pairs per register
+    constexpr bool kRing8 = SGM_FUSE_RING8 < 0 ? R <= 9 : SGM_FUSE_RING8 != 0;
+    constexpr bool kEarly = SGM_FUSE_BOX_EARLY < 0 ? R <= 9 : SGM_FUSE_BOX_EARLY != 0;
+    constexpr int RQ = kRing8 ? I / 2 : I;
+    uint32_t ring[RQ][R];
     uint32_t Vs[I];
 #pragma unroll
-    for (int q = 0; q < I; q++) {
-        Vs[q] = 0;
+    for (int q = 0; q < I; q++) Vs[q] = 0;
+#pragma unroll
+    for (int q = 0; q < RQ; q++)
 #pragma unroll
         for (int s2 = 0; s2 < R; s2++) ring[q][s2] = 0;
-    }
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
     // box: thread (segment, pair); NB box threads, L outputs per segment, the NL = L + R - 1
@@ -613,7 +625,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
         // computed (independent LDS buffers), so their latency hides behind that work
         const bool dobox = t < NB && v >= 1 && v - 1 >= 2 * SH2 && xa < xb;
         u16x2_t w[NL];
-        if constexpr (SGM_FUSE_BOX_EARLY)
+        if constexpr (kEarly)
             if (dobox) box_load(w);
         if (v < nv) {
             const uint32_t* Lk = S + 6 * kc;
@@ -637,11 +649,24 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             }
             auto upd = [&](auto ss) {
                 constexpr int s2 = decltype(ss)::value;
-#pragma unroll
-                for (int q = 0; q < I; q++) {
+                auto vupd = [&](int q, uint32_t old) {
                     Vs[q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_t, Vs[q]) + __builtin_bit_cast(u16x2_t, P[q]) -
-                                                         __builtin_bit_cast(u16x2_t, ring[q][s2]));
-                    ring[q][s2] = P[q];
+                                                         __builtin_bit_cast(u16x2_t, old));
+                };
+                if constexpr (kRing8) {
+#pragma unroll
+                    for (int h = 0; h < RQ; h++) {
+                        const uint32_t o = ring[h][s2];
+                        vupd(2 * h, __builtin_amdgcn_perm(o, o, 0x0C010C00u));       // bytes 0, 1 -> u16 lanes
+                        vupd(2 * h + 1, __builtin_amdgcn_perm(o, o, 0x0C030C02u));   // bytes 2, 3
+                        ring[h][s2] = __builtin_amdgcn_perm(P[2 * h + 1], P[2 * h], 0x06040200u);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < I; q++) {
+                        vupd(q, ring[q][s2]);
+                        ring[q][s2] = P[q];
+                    }
                 }
             };
             switch (slot) {
@@ -663,7 +688,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
         if (dobox) {                                         // the box of row v - 1
             const int y = y0 + (v - 1) - 2 * SH2;
             const bool tail = last_band && y == fg_ncomp - 1;
-            if constexpr (!SGM_FUSE_BOX_EARLY) box_load(w);
+            if constexpr (!kEarly) box_load(w);
             u16x2_t sum = w[0];
 #pragma unroll
             for (int i = 1; i < R; i++) sum += w[i];
@@ -722,7 +747,7 @@ __host__ inline bool ocv_cost_fusable(const Geom& g)
     // fused vs 0.053 ms; 1080p block 5 0.29 vs 0.42, the shipped block-21 config 3.18 vs 3.79 ms,
     // profiles/r04_ocv_cost_box_ab.jsonl)
     const bool dflt = (double)g.width1 * g.H * g.D >= 1e8;
-    return g.SH2 <= 10 && g.SW2 == g.SH2 && B <= 65535 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
+    return g.SH2 <= 10 && g.SW2 == g.SH2 && B <= 65535 && 2 * g.ftzero + 63 <= 255 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
 }
 
 // The SIMD_SAT flagged frames whose horizontal sums cannot saturate: when

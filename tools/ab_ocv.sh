@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: interleaved A/B of the OpenCV-mode timings (tools/ocv_modes_bench.py). A variant is
 # a library built by tools/build_variant.sh (SGM_HIP_LIB), "base" (the in-tree one) or an
-# environment assignment NAME=VALUE run with the in-tree library.
+# environment assignment NAME=VALUE run with the in-tree library, or VARIANT+NAME=VALUE (both).
 #   bash tools/ab_ocv.sh CASE_SUBSTRING ROUNDS variant1 variant2 ...
 set -u
 CASE=$1; R=$2; shift 2
@@ -11,6 +11,7 @@ for r in $(seq 1 $R); do
     lib=""; envv=""
     case $v in
       base) ;;
+      *+*=*) lib=i3dr_stereo_camera-ros_amd/lib/variants/${v%%+*}/libsgm_hip.so; envv=${v#*+} ;;
       *=*) envv=$v ;;
       *) lib=i3dr_stereo_camera-ros_amd/lib/variants/$v/libsgm_hip.so ;;
     esac
