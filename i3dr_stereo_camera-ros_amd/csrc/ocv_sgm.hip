@@ -478,23 +478,24 @@ struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
 };
 template <int R, int DPC, int I>
-// A/B knobs of k_ocv_cost_fused (-1: the measured default, by box size R; profiles/r04_ocv_cost_ring_ab.jsonl:
-// R <= 9 (1080p block 5) 0.302 -> 0.239 ms with both on, two blocks per CU at 113 VGPRs; R = 21 (the shipped
-// block 21) 3.18 ms with both off against 3.61 (ring bytes) / 4.58 (early box reads): one block per CU either
-// way, where the extra registers and repacking only add work)
+// A/B knobs of k_ocv_cost_fused, defaults as measured (profiles/r04_ocv_cost_ring_ab_v2.jsonl; cost stage,
+// 1080p block 5 / the shipped 2448x2048 D=480 block 21): the ring as bytes 0.234 -> 0.231 / 3.17 -> 3.01 ms,
+// plus <= 128 VGPRs asked for R > 9 (two blocks per CU at 36 B of spills) -> 2.86 ms; the box reads issued
+// before the pixel costs instead of after the V store: 3.73 ms at R = 21 (the window registers live across
+// the pixel-cost phase), no gain at R = 5
 #ifndef SGM_FUSE_RING8
-#define SGM_FUSE_RING8 -1        // the pixel-cost ring as bytes (half the registers)
+#define SGM_FUSE_RING8 1         // the pixel-cost ring as bytes (half the registers)
 #endif
 #ifndef SGM_FUSE_BOX_EARLY
-#define SGM_FUSE_BOX_EARLY -1    // the box reads issued before the pixel costs (else after the V store)
+#define SGM_FUSE_BOX_EARLY 0     // the box reads issued before the pixel costs (else after the V store)
 #endif
 #ifndef SGM_FUSE_NB_WIDE
 #define SGM_FUSE_NB_WIDE 256     // A/B: box threads for R > 9 (512: every wave)
 #endif
 #ifndef SGM_FUSE_WPE
-#define SGM_FUSE_WPE 1           // A/B: waves per SIMD asked of the compiler (4: <= 128 VGPRs, two blocks per CU)
+#define SGM_FUSE_WPE -1          // waves per SIMD asked of the compiler (4: <= 128 VGPRs); -1: 4 for R > 9
 #endif
-__global__ __launch_bounds__(kFuseThreads) __attribute__((amdgpu_waves_per_eu(SGM_FUSE_WPE)))
+__global__ __launch_bounds__(kFuseThreads) __attribute__((amdgpu_waves_per_eu(SGM_FUSE_WPE < 0 ? (R > 9 ? 4 : 1) : SGM_FUSE_WPE)))
 void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                                                                  FuseGrid fg, int16_t* __restrict__ C)
 {
@@ -566,8 +567,8 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     const int kc = t / TPC, tq = t % TPC;
     // kRing8: a pixel cost is <= 2*ftzero + 63 <= 255 (the launcher's condition), so the ring
     // keeps bytes, two disparity pairs per register
-    constexpr bool kRing8 = SGM_FUSE_RING8 < 0 ? R <= 9 : SGM_FUSE_RING8 != 0;
-    constexpr bool kEarly = SGM_FUSE_BOX_EARLY < 0 ? R <= 9 : SGM_FUSE_BOX_EARLY != 0;
+    constexpr bool kRing8 = SGM_FUSE_RING8 != 0;
+    constexpr bool kEarly = SGM_FUSE_BOX_EARLY != 0;
     constexpr int RQ = kRing8 ? I / 2 : I;
     uint32_t ring[RQ][R];
     uint32_t Vs[I];
@@ -704,10 +705,19 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 o += gD / 2;
             }
             if (tail) {                                      // OpenCV's bottom rows: never recomputed
+                // (the row's values slid again from the registers: reading the stores back would
+                // put a vmcnt(0) wait into every row of the loop)
+                sum = w[0];
+#pragma unroll
+                for (int i = 1; i < R; i++) sum += w[i];
                 o = o0;
-                for (int xo = xa; xo < xb; xo++, o += gD / 2) {
-                    const uint32_t c = fullDP ? gP2 * 0x10001u : o[0];   // this thread's own store
-                    for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
+#pragma unroll
+                for (int j = 0; j < L; j++) {
+                    if (j > 0) sum += w[j + R - 1] - w[j - 1];
+                    const uint32_t c = fullDP ? gP2 * 0x10001u : __builtin_bit_cast(uint32_t, sum + p2v);
+                    if (xa + j < xb)
+                        for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
+                    o += gD / 2;
                 }
             }
         }
