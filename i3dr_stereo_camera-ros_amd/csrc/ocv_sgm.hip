@@ -36,6 +36,11 @@ constexpr int kMaxCost = 32767;
 #ifndef SGM_OCV_VWTA_PF
 #define SGM_OCV_VWTA_PF 3    // steps whose operands k_ocv_vwta keeps in flight (DPL <= 8)
 #endif
+#ifndef SGM_OCV_VWTA_RL
+#define SGM_OCV_VWTA_RL 0    // k_ocv_vwta: S[best +- 1] by one readlane per element (0: select, then one readlane;
+                             // the select is folded into an LDS-indexed load, 86 % bank-conflict cycles, but the
+                             // kernel is memory-bound: 3.67 vs 3.66 ms, profiles/r04_ocv_vwta_rl_ab.jsonl)
+#endif
 #ifndef SGM_OCV_PF_WIDE32
 #define SGM_OCV_PF_WIDE32 4  // 32-lane lines with more than 4 values per lane (D > 256: the shipped
                              // 2448x2048 D=480 config, 1 / 2 / 3 / 4 rows: MODE_SGBM 15.01 / 14.86 /
@@ -1503,9 +1508,10 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
         // every S saturated at MAX_COST: bestDisp stays -1 in OpenCV (see k_ocv_wta16)
         const bool rej = __ballot(hit) != 0ull || minS >= 32767;
         auto s_at = [&](int d) {                       // S[d] of the pixel (d wave-uniform)
+            const int kk = d % DPL, ln = d / DPL;
+#if SGM_OCV_VWTA_RL
             // one readlane per element, the element picked among the scalars: a select over the
             // S registers themselves is folded into an indexed load, which puts S in LDS
-            const int kk = d % DPL, ln = d / DPL;
             int v = __builtin_amdgcn_readlane(S[0], ln);
 #pragma unroll
             for (int k = 1; k < DPL; k++) {
@@ -1513,6 +1519,12 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
                 v = kk == k ? r : v;
             }
             return v;
+#else
+            int v = S[0];
+#pragma unroll
+            for (int k = 1; k < DPL; k++) v = kk == k ? S[k] : v;
+            return __builtin_amdgcn_readlane(v, ln);
+#endif
         };
         const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, g.D - 1));
         const int den = max(sm + sp - 2 * minS, 1);
