@@ -541,15 +541,17 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     const int cr0 = st >= NRr, r0 = st - cr0 * NRr;
     const bool has1 = st + 256 < 2 * NRr;
     const int cr1 = st + 256 >= NRr, r1 = st + 256 - cr1 * NRr;
-    const uint32_t* btL = bt + cl * plane + min(max(xs + kl, 0), gW - 1);
-    const uint32_t* btR0 = bt + (2 + cr0) * plane + min(max(xr0 + r0, 0), gW - 1);
-    const uint32_t* btR1 = bt + (2 + cr1) * plane + min(max(xr0 + r1, 0), gW - 1);
+    // 32-bit element offsets off the uniform base (4 planes < 2^32 elements: the launcher's
+    // condition), one register each instead of a 64-bit pointer
+    const uint32_t oL = (uint32_t)(cl * plane) + (uint32_t)min(max(xs + kl, 0), gW - 1);
+    const uint32_t oR0 = (uint32_t)((2 + cr0) * plane) + (uint32_t)min(max(xr0 + r0, 0), gW - 1);
+    const uint32_t oR1 = (uint32_t)((2 + cr1) * plane) + (uint32_t)min(max(xr0 + r1, 0), gW - 1);
     uint32_t wl = 0, wr0 = 0, wr1 = 0;
     auto stage_load = [&](int v) {
-        const size_t ro = (size_t)min(max(y0 - SH2 + v, 0), gH - 1) * gW;
-        wl = btL[ro];
-        wr0 = btR0[ro];
-        wr1 = has1 ? btR1[ro] : 0u;
+        const uint32_t ro = (uint32_t)(min(max(y0 - SH2 + v, 0), gH - 1) * gW);
+        wl = bt[oL + ro];
+        wr0 = bt[oR0 + ro];
+        wr1 = has1 ? bt[oR1 + ro] : 0u;
     };
     auto put_right = [&](uint16_t* Rh, int c, int r, uint32_t w) {
         const int j = M - 1 - r;
@@ -698,16 +700,16 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             u16x2_t sum = w[0];
 #pragma unroll
             for (int i = 1; i < R; i++) sum += w[i];
-            uint32_t* const o0 = C32 + (size_t)y * rowC + ((size_t)(x0 + xa) * gD + d0) / 2 + bp;
-            uint32_t* o = o0;
+            // 32-bit element offsets off the uniform C' base (C' < 2^32 words: the launcher's
+            // condition): one register per store instead of a 64-bit address
+            const uint32_t ob = (uint32_t)y * (uint32_t)rowC + (uint32_t)(((x0 + xa) * gD + d0) / 2 + bp);
 #pragma unroll
             for (int j = 0; j < L; j++) {
                 if (j > 0) sum += w[j + R - 1] - w[j - 1];
                 if (xa + j < xb) {
                     if (!(col0 && xa + j == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
-                    o[0] = __builtin_bit_cast(uint32_t, sum + p2v);
+                    C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum + p2v);
                 }
-                o += gD / 2;
             }
             if (tail) {                                      // OpenCV's bottom rows: never recomputed
                 // (the row's values slid again from the registers: reading the stores back would
@@ -715,7 +717,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 sum = w[0];
 #pragma unroll
                 for (int i = 1; i < R; i++) sum += w[i];
-                o = o0;
+                uint32_t* o = C32 + ob;
 #pragma unroll
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
@@ -762,7 +764,8 @@ __host__ inline bool ocv_cost_fusable(const Geom& g)
     // fused vs 0.053 ms; 1080p block 5 0.29 vs 0.42, the shipped block-21 config 3.18 vs 3.79 ms,
     // profiles/r04_ocv_cost_box_ab.jsonl)
     const bool dflt = (double)g.width1 * g.H * g.D >= 1e8;
-    return g.SH2 <= 10 && g.SW2 == g.SH2 && B <= 65535 && 2 * g.ftzero + 63 <= 255 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
+    return g.SH2 <= 10 && g.SW2 == g.SH2 && B <= 65535 && 2 * g.ftzero + 63 <= 255 &&
+           (double)g.W * g.H * 4 < 4294967296.0 && (double)g.width1 * g.H * g.D / 2 < 4294967296.0 && g.width1 > 0 && (e ? std::atoi(e) != 0 : dflt);
 }
 
 // The SIMD_SAT flagged frames whose horizontal sums cannot saturate: when
