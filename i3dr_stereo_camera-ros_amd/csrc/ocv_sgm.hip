@@ -1603,9 +1603,24 @@ static FuseGrid fuse_grid(const Geom& g)
     fg.chunks = g.D / (2 * dpc);
     fg.ncomp = std::max(g.H - g.SH2 - 1, 0) + 1;             // rows 0 .. ylast are computed
     const long long tiles = (long long)fg.strips * fg.chunks;
+    // bands: about four rounds of blocks over the chip's slots (two 512-thread blocks per CU, every
+    // instantiation at <= 128 VGPRs), bands of about max(64, 8*SH2) rows or more so the 2*SH2
+    // warm-up rows stay a small share. Measured (profiles/r04_ocv_cost_rows_ab.jsonl): the shipped block-21
+    // config 2.43 ms at the earlier ~ncomp*tiles/1024 rows (507: 1275 blocks, 2.5 rounds) against
+    // 2.06 at 256 rows (2040 blocks), 2.10-2.11 at 128-160; 1080p block 5 best at 64 rows
+    static int slots = 0;
+    if (!slots) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        slots = 2 * cus;
+    }
+    const int min_rows = std::max(64, 8 * g.SH2);
+    const long long nb = std::max<long long>(1, std::min<long long>((4LL * slots + tiles / 2) / std::max(tiles, 1LL),
+                                                                    (fg.ncomp + min_rows - 1) / min_rows));
     const char* e = std::getenv("SGM_FUSE_ROWS");
-    fg.band_rows = e ? std::max(std::atoi(e), 1)
-                     : (int)std::max<long long>(std::max(64, 8 * g.SH2), (fg.ncomp * tiles + 1023) / 1024);
+    fg.band_rows = e ? std::max(std::atoi(e), 1) : (int)((fg.ncomp + nb - 1) / nb);
     fg.bands = (fg.ncomp + fg.band_rows - 1) / fg.band_rows;
     fg.total = (int)(tiles * fg.bands);
     fg.per_xcd = (fg.total + 7) / 8;

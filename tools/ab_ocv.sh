@@ -11,6 +11,7 @@ for r in $(seq 1 $R); do
     lib=""; envv=""
     case $v in
       base) ;;
+      base+*=*) envv=${v#*+} ;;
       *+*=*) lib=i3dr_stereo_camera-ros_amd/lib/variants/${v%%+*}/libsgm_hip.so; envv=${v#*+} ;;
       *=*) envv=$v ;;
       *) lib=i3dr_stereo_camera-ros_amd/lib/variants/$v/libsgm_hip.so ;;
