@@ -473,8 +473,12 @@ struct FuseGeo {
         DC = 2 * dpc;
         M = ((kFuseNX + DC) & ~1) + 2;
         MH = M / 2;
+        // 32 pairs per block: the odd-entry half starts at MH = 101 (not 97), which makes the
+        // pixel-cost reads of a 32-lane half hit 32 distinct banks (2-way before: SQ_LDS_BANK_CONFLICT
+        // 44 % of the LDS cycles at 1080p block 5, profiles/r04_ocv_cost_pmc_fused_final_1080p.txt)
+        if (dpc == 32) MH += ((5 - MH % 8) + 8) % 8;
     }
-    __host__ __device__ int stage_words() const { return 6 * kFuseNX + 7 * M; }
+    __host__ __device__ int stage_words() const { return 6 * kFuseNX + 14 * MH; }
     __host__ __device__ size_t lds_bytes(int dpc) const {
         return (size_t)4 * (2 * stage_words() + 2 * kFuseNX * dpc);
     }
