@@ -19,6 +19,7 @@
 // overflow flag ("OpenCV semantics targets").
 #include "sgm_device.h"
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 namespace sgm {
@@ -693,8 +694,15 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             slot = slot + 1 == R ? 0 : slot + 1;
             if (v >= 2 * SH2) {
                 uint32_t* Vout = V0 + (v & 1) * NX * DPC + kc * DPC + tq * I;
+                // exactly the thread's I words (I = 2 at DPC = 8: one 8-byte store, 8-byte aligned)
+                if constexpr (I % 4 == 0) {
 #pragma unroll
-                for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
+                    for (int q = 0; q < I; q += 4) *(uint4*)(Vout + q) = make_uint4(Vs[q], Vs[q + 1], Vs[q + 2], Vs[q + 3]);
+                } else {
+                    static_assert(I % 2 == 0, "pairs of words per thread");
+#pragma unroll
+                    for (int q = 0; q < I; q += 2) *(uint2*)(Vout + q) = make_uint2(Vs[q], Vs[q + 1]);
+                }
             }
         }
         if (dobox) {                                         // the box of row v - 1
@@ -1612,13 +1620,18 @@ static FuseGrid fuse_grid(const Geom& g)
     // warm-up rows stay a small share. Measured (profiles/r04_ocv_cost_rows_ab.jsonl): the shipped block-21
     // config 2.43 ms at the earlier ~ncomp*tiles/1024 rows (507: 1275 blocks, 2.5 rounds) against
     // 2.06 at 256 rows (2040 blocks), 2.10-2.11 at 128-160; 1080p block 5 best at 64 rows
-    static int slots = 0;
+    // slot count of the calling thread's current device, cached per device (launches run from
+    // several host threads at once: per-device atomics, each written with the same value)
+    static std::atomic<int> slots_of[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    int slots = dev < 64 ? slots_of[dev].load(std::memory_order_relaxed) : 0;
     if (!slots) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
         slots = 2 * cus;
+        if (dev < 64) slots_of[dev].store(slots, std::memory_order_relaxed);
     }
     const int min_rows = std::max(64, 8 * g.SH2);
     const long long nb = std::max<long long>(1, std::min<long long>((4LL * slots + tiles / 2) / std::max(tiles, 1LL),
@@ -1639,13 +1652,21 @@ static FuseGrid fuse_grid(const Geom& g)
 // plain horizontal sums (k_ocv_vsum_sat2; after the fused cost, a gated k_ocv_pixhsum makes
 // those sums first) when the horizontal sums cannot saturate, else the sequential chain
 // (pixel costs -> bufA, horizontal sums -> bufB, C' -> bufA).
+// The frame's cost stage takes k_ocv_cost_fused (and so reads the packed BT planes after the
+// prefilter planes): the workspace layout reserves those 16 B/px only then.
+// wide == 1 with SIMD_SAT: every launch after the cost reads the SIMD cost, the plain C' is never used.
+bool ocv_cost_takes_fused(const Geom& g)
+{
+    const bool simd_only = g.wide == 1 && (g.compat & SGM_OCV_SIMD_SAT);
+    return !simd_only && ocv_cost_fusable(g);
+}
+
 hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, const Geom& g, int fullDP,
                            uint8_t* planes, int16_t* bufA, int16_t* bufB, hipStream_t st)
 {
     const size_t lds = pix_lds_bytes(g);
-    // wide == 1 with SIMD_SAT: every launch after this one reads the SIMD cost, the plain C' is never used
     const bool simd_only = g.wide == 1 && (g.compat & SGM_OCV_SIMD_SAT);
-    const bool fused = !simd_only && ocv_cost_fusable(g);
+    const bool fused = ocv_cost_takes_fused(g);
     uint32_t* bt = fused ? (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H)) : nullptr;
     hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes, bt);

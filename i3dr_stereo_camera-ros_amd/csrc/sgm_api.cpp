@@ -47,6 +47,7 @@ hipError_t launch_depth_points(const float*, size_t, int, int, const float*, dou
                                int, float*, size_t, float4*, int, int*, int*, hipStream_t);
 hipError_t launch_ocv_cost(const uint8_t*, const uint8_t*, size_t, const Geom&, int, uint8_t*, int16_t*, int16_t*,
                            hipStream_t);
+bool ocv_cost_takes_fused(const Geom&);
 hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const Geom&, int, hipStream_t,
                             int skipdir = -1);
 hipError_t launch_ocv_vwta(const int16_t*, const int16_t*, const void*, size_t, int, const Geom&, uint64_t*, hipStream_t);
@@ -363,7 +364,8 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
             }
         }
     } else {
-        l.planes = take(sgm::ocv_planes_total(g.W, g.H));
+        // the packed BT planes (16 B/px) only for frames whose cost stage takes the fused kernel
+        l.planes = take(sgm::ocv_cost_takes_fused(g) ? sgm::ocv_planes_total(g.W, g.H) : sgm::ocv_planes_bytes(g.W, g.H));
         l.bufA = take(cells * 2);
         l.bufB = take(cells * 2);
         const size_t es = g.wide && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // int32 / int16 path volumes
@@ -943,7 +945,13 @@ int sgm_host_register(sgm_handle* h, void* ptr, size_t bytes)
     if (!h) return SGM_ERR_ARG;
     if (!ptr || !bytes) return fail(h, SGM_ERR_ARG, "null or empty host range");
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
+    // a failed registration is not fatal to the caller (it falls back to pageable copies), so
+    // HIP's last error is cleared here: the next launcher's hipGetLastError must not report it
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return hip_fail(h, e, "hipHostRegister");
+    }
     return SGM_OK;
 }
 
@@ -952,7 +960,11 @@ int sgm_host_unregister(sgm_handle* h, void* ptr)
     if (!h) return SGM_ERR_ARG;
     if (!ptr) return fail(h, SGM_ERR_ARG, "null host pointer");
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-    HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return hip_fail(h, e, "hipHostUnregister");
+    }
     return SGM_OK;
 }
 

@@ -83,6 +83,36 @@ def test_fuzz_match(engine, oracle, synth, pkg, seed):
     assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
 
 
+def _ocv_fusable(h, w, kw):
+    """ocv_cost_fusable() of csrc/ocv_sgm.hip without its size default (forced below)."""
+    ftzero = max(kw["prefilter_cap"], 15) | 1
+    block, minD, D = kw["block_size"], kw["min_disparity"], kw["num_disparities"]
+    width1 = (w + min(minD, 0)) - max(minD + D, 0)
+    return block // 2 <= 10 and block * block * (2 * ftzero + 63) <= 65535 and width1 > 0
+
+
+@pytest.mark.parametrize("seed", [s for s in range(N_CASES) if s % 3])   # the OpenCV-mode cases
+def test_fuzz_ocv_fused_cost(engine, oracle, synth, pkg, monkeypatch, seed):
+    """Every OpenCV-mode case of test_fuzz_match again with the fused cost kernel forced
+    (SGM_OCV_FUSED=1; the default only on frames of >= 10^8 cells) at a drawn disparity-pair
+    block width (SGM_FUSE_DPC 8 / 16 / 32, falling back as the launcher does) and band height
+    (SGM_FUSE_ROWS). Cases the kernel cannot take (boxes above 21, u16 box sums that could
+    wrap, no valid column) run the unfused kernels and still must match."""
+    rng, mode, h, w, kw, kind = _case(pkg, seed)
+    sub = np.random.default_rng(70_000 + seed)
+    monkeypatch.setenv("SGM_OCV_FUSED", "1")
+    monkeypatch.setenv("SGM_FUSE_DPC", str(int(sub.choice([8, 16, 32]))))
+    if sub.random() < 0.5:
+        monkeypatch.setenv("SGM_FUSE_ROWS", str(int(sub.choice([1, 3, 16, 64]))))
+    p = pkg.default_params(mode, **kw)
+    engine.set_params(p)
+    left, right = _images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    tag = "fused" if _ocv_fusable(h, w, kw) else "unfused"
+    assert np.array_equal(got, ref), f"[{tag}] mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
+
+
 @pytest.mark.parametrize("seed", range(0, N_CASES, 3))        # the census cases
 def test_fuzz_device_batch(engine, oracle, synth, pkg, seed):
     torch = pytest.importorskip("torch")

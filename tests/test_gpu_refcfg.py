@@ -65,6 +65,24 @@ def test_reference_config_gate_takes_int32_on_overflow(engine, oracle, pkg, mode
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_reference_config_full_frame_vs_oracle(engine, oracle, pkg, ref_frame, mode):
+    """The whole shipped 2448 x 2048 frame (minD 147, D 480, block 21) under the default melodic
+    build against the oracle, bit for bit: the default path end to end at its production size —
+    the fused cost kernel's full band / strip layout (k_ocv_cost_fused<21, 16, 4>), the 32-bit
+    buffer-offset path kernel over 3.6 GB volumes, the fused vertical path + WTA, median and
+    speckles. (The oracle takes about a minute per mode here.)"""
+    left, right, _ = ref_frame
+    p = _params(pkg, mode)
+    assert p.ocv_compat == pkg.COMPAT_MELODIC
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    assert (ref != (147 - 1) * 16).mean() > 0.5
+
+
 @pytest.mark.parametrize("mode", ["sgbm", "hh"])
 def test_reference_config_full_frame_properties(engine, pkg, ref_frame, mode, monkeypatch):
     """The whole 2448 x 2048 frame (the CPU oracle takes minutes at this size): repeatable,
