@@ -240,7 +240,7 @@ def launch_ranks(n, argv, dry_run=False):
     rank succeeded, else the first failing rank's code (the others are terminated)."""
     if not dry_run:
         vis = visible_devices()
-        if vis < n:
+        if vis < (1 if "--share-device" in argv else n):
             print(f"bench.py: --gpus {n} but only {vis} HIP device(s) visible", file=sys.stderr)
             return 2
     port = free_port()
@@ -419,6 +419,9 @@ def main():
     ap.add_argument("--c5-frames", type=int, default=10, help="timed C5 frames of the default run's c5 block")
     ap.add_argument("--c5-timeout", type=int, default=300)
     ap.add_argument("--c5-only", action="store_true", help=argparse.SUPPRESS)
+    # test-only: every rank on device 0 over gloo (RCCL cannot put two ranks on one GPU), so the
+    # N > 1 path (launcher -> ranks -> HIP engine -> MAX -> one line) runs on a one-GPU box
+    ap.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -445,14 +448,19 @@ def main():
 
     distributed = world > 1
     n_vis = torch.cuda.device_count()
-    need = max(world, args.gpus if args.config == "c5" else 1)
+    need = 1 if args.share_device else max(world, args.gpus if args.config == "c5" else 1)
+    if args.share_device:
+        local_rank = 0
     if n_vis < need or local_rank >= n_vis:
         print(f"bench.py: needs {need} HIP device(s) (rank {rank}, local rank {local_rank}), {n_vis} visible",
               file=sys.stderr)
         sys.exit(2)
     if distributed:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
     device = torch.cuda.current_device()
@@ -549,7 +557,7 @@ def main():
     n_prof = eng.profiled_matches()
     eng.set_profiling(False)
 
-    elapsed_max = max_over_ranks(elapsed, device)
+    elapsed_max = max_over_ranks(elapsed, None if args.share_device else device)
     shard = gather_shard(ids, elapsed, distributed)
 
     # single-frame latency beside the batch throughput (BASELINE's C2 is quoted as a single
@@ -634,6 +642,7 @@ def main():
                        "frames_per_rank_per_step": args.frames, "global_batch": args.frames * world,
                        "distinct_frames_per_rank": args.distinct, "parallelism": f"frame-shard x{world}",
                        "frame_pipeline": not args.no_pipeline, "rectify_fused": bool(args.rectify),
+                       **({"shared_device_test": True} if args.share_device else {}),
                        "host_io": bool(args.host_io)},
             "roofline": roofline,
             "pipeline": pipeline,

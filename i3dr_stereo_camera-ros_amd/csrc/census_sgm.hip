@@ -878,9 +878,9 @@ __device__ __forceinline__ void wta_emask(int p, const Geom& g, uint32_t (&emask
 }
 
 // One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
-template <int DPL, bool EXACT>
+template <int DPL, bool EXACT, typename OutT = int16_t>
 __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size_t vol_bytes, const Geom& g,
-                                          int16_t* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
+                                          OutT* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
 {
     constexpr int NWD = (DPL + 3) / 4;            // dwords per lane per volume
     uint32_t* sl = lds;                           // 4 waves x 4 rows x 16 lanes x 2*NWD packed S dwords
@@ -963,6 +963,17 @@ __global__ __launch_bounds__(kWG) void k_census_wta16(WtaFrames wf, size_t vol_b
 {
     extern __shared__ uint32_t lds_dyn[];
     wta_block16<DPL, EXACT>(wf, vol_bytes, g, out_stride, blockIdx.x, lds_dyn);
+}
+
+// The same for one frame whose rows go out as float (the node's CV_32FC1) straight into a host
+// buffer mapped into the device's address space: the row stores cross PCIe while the other rows'
+// volume reads run, instead of a to-float kernel and an 8 MB copy after the frame (the node's
+// host call, matcherOpenCVSGBM.cpp:34 / generate_disparity.cpp:350-357).
+template <int DPL, bool EXACT>
+__global__ __launch_bounds__(kWG) void k_census_wta16f(WtaFrames wf, size_t vol_bytes, Geom g)
+{
+    extern __shared__ uint32_t lds_dyn[];
+    wta_row16<DPL, EXACT, float>(wf.vols[0], vol_bytes, g, wf.outf[0], wf.outf_stride, blockIdx.x, lds_dyn);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1262,6 +1273,13 @@ static void launch_wta_dpl(const WtaFrames& wf, size_t vol_bytes, const Geom& g,
 {
     dim3 grid(g.H * wf.n), block(kWG);
     const size_t lds = wta_lds_bytes<DPL>(g.W);
+    if (wf.outf[0]) {                  // one frame, float rows into a mapped host buffer
+        if (g.D == 16 * DPL)
+            hipLaunchKernelGGL((k_census_wta16f<DPL, true>), dim3(g.H), block, lds, st, wf, vol_bytes, g);
+        else
+            hipLaunchKernelGGL((k_census_wta16f<DPL, false>), dim3(g.H), block, lds, st, wf, vol_bytes, g);
+        return;
+    }
     if (g.D == 16 * DPL)
         hipLaunchKernelGGL((k_census_wta16<DPL, true>), grid, block, lds, st, wf, vol_bytes, g, out_stride);
     else

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -56,6 +57,14 @@ hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_
 }  // namespace sgm
 
 using sgm::Geom;
+
+// measurement-only build knobs (tools/build_variant.sh ... sgm_api.cpp)
+#ifndef SGM_VOL_PAD_BYTES
+#define SGM_VOL_PAD_BYTES 0    // extra bytes per census volume slot
+#endif
+#ifndef SGM_IO_PRIO
+#define SGM_IO_PRIO 1          // host-I/O copy streams at the highest stream priority
+#endif
 
 namespace {
 
@@ -189,6 +198,12 @@ struct sgm_handle {
     size_t io_pin_size = 0;
     hipStream_t up = nullptr, down = nullptr;
     std::vector<hipEvent_t> io_ev;
+    // host buffers page-locked and mapped by sgm_host_register (host range -> device address)
+    struct HostReg { char* host; size_t bytes; char* dev; };
+    std::vector<HostReg> regs;
+    // host-buffer matches: the right image's copy runs on `cpy` beside the left image's census
+    hipStream_t cpy = nullptr;
+    hipEvent_t cpy_ev = nullptr;
 };
 
 namespace {
@@ -340,9 +355,10 @@ Layout make_layout(const sgm_params& p, const Geom& g, bool host_io, int group =
     const size_t cells = (size_t)std::max(g.width1, 0) * g.H * g.D;
     if (p.mode == SGM_MODE_CENSUS8) {
         l.vol_bytes = align_up(cells + kTrashBytes);   // + trash slot for masked stores
-        // extra bytes per volume slot (a measurement knob): clamped to [0, 1 GiB]
-        if (const char* e = std::getenv("SGM_VOL_PAD"))
-            l.vol_bytes = align_up(l.vol_bytes + (size_t)std::min(std::max(std::atoll(e), 0LL), 1LL << 30));
+#if SGM_VOL_PAD_BYTES > 0
+        // extra bytes per volume slot (a measurement build: tools/build_variant.sh, -DSGM_VOL_PAD_BYTES=N)
+        l.vol_bytes = align_up(l.vol_bytes + (size_t)std::min<long long>(SGM_VOL_PAD_BYTES, 1LL << 30));
+#endif
         l.group = std::max(group, 1);
         // D > 256 (32 disparities per lane, 2 waves/SIMD) keeps the earlier scheme: its up+WTA
         // blocks are long latency-bound chains (C5 batch: 32.3 vs 23.3 ms per frame)
@@ -474,8 +490,15 @@ bool ocv_vwta_on(const Geom& g, int fullDP)
 }
 
 // Runs the whole pipeline on device buffers, asynchronously on h->stream.
+// copy_r (census mode): dR is not written yet; the left image's census is launched first, then
+// copy_r() issues the right image's copy and returns the event that completes it, and the right
+// image's census waits on that event (a pageable copy can hold the host until it is done, so the
+// left census must already be queued). outf (census mode without median / speckles): the WTA
+// writes the final rows as float to outf (a mapped host buffer, row stride outf_stride floats)
+// and dOut is not written.
 int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* dL, const uint8_t* dR, size_t stride,
-                 int16_t* dOut, size_t out_stride)
+                 int16_t* dOut, size_t out_stride, const std::function<hipEvent_t()>& copy_r = nullptr,
+                 float* outf = nullptr, size_t outf_stride = 0)
 {
     const sgm_params& p = h->params;
     char* ws = (char*)h->ws.base;
@@ -497,7 +520,15 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         uint64_t* cR = (uint64_t*)(ws + l.cR[0]);
         uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
         rec.begin("census", 2 * WH + 16 * WH);
-        HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
+        if (copy_r) {
+            HIP_TRY(sgm::launch_census(dL, nullptr, stride, g.W, g.H, cL, nullptr, st), "census L");
+            const hipEvent_t r_ready = copy_r();
+            if (!r_ready) return SGM_ERR_DEVICE;
+            HIP_TRY(hipStreamWaitEvent(st, r_ready, 0), "hipStreamWaitEvent");
+            HIP_TRY(sgm::launch_census(dR, nullptr, stride, g.W, g.H, cR, nullptr, st), "census R");
+        } else {
+            HIP_TRY(sgm::launch_census(dL, dR, stride, g.W, g.H, cL, cR, st), "census");
+        }
         const uint32_t* items;
         const int n_items = path_items(h, l, g, 0xFFu, 1, st, &items);
         if (n_items < 0) return n_items;
@@ -505,6 +536,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
         sgm::WtaFrames wf{};
         wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
+        if (outf) { wf.outf[0] = outf; wf.outf_stride = outf_stride; }
         rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
@@ -835,11 +867,46 @@ int match_host(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, int H, 
     hipStream_t st = h->stream;
     const size_t es = f32 ? 4 : 2;
     char* ws = (char*)h->ws.base;
+    const sgm_params& p = h->params;
+    const bool census = p.mode == SGM_MODE_CENSUS8 && g.width1 > 0;
+    // census mode: the left image's census runs while the right image is copied (second stream)
+    if (census) {
+        if (!h->cpy) HIP_TRY(hipStreamCreateWithFlags(&h->cpy, hipStreamNonBlocking), "hipStreamCreate");
+        if (!h->cpy_ev) HIP_TRY(hipEventCreateWithFlags(&h->cpy_ev, hipEventDisableTiming), "hipEventCreate");
+        HIP_TRY(hipEventRecord(h->cpy_ev, st), "hipEventRecord");        // the workspace is free
+        HIP_TRY(hipStreamWaitEvent(h->cpy, h->cpy_ev, 0), "hipStreamWaitEvent");
+    }
     HIP_TRY(hipMemcpy2DAsync(ws + l.inL, W, L, stride, W, H, hipMemcpyHostToDevice, st), "H2D L");
-    HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
+    // f32 output that is the WTA's own (census, no median / speckles) into a registered, mapped
+    // host buffer: the WTA writes the float rows there itself (no to-float pass, no copy back)
+    float* outf = nullptr;
+    if (f32 && census && !use_median(p) && p.speckle_window_size <= 0) {
+        const size_t need = out_stride * 4 * (size_t)(H - 1) + (size_t)W * 4;
+        for (const auto& r : h->regs)
+            if (r.dev && (char*)out >= r.host && (char*)out + need <= r.host + r.bytes) {
+                outf = (float*)(r.dev + ((char*)out - r.host));
+                break;
+            }
+    }
     int16_t* d16 = (int16_t*)(ws + l.out);
-    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W);
+    std::function<hipEvent_t()> copy_r;
+    if (census) {
+        copy_r = [&]() -> hipEvent_t {
+            hipError_t e = hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, h->cpy);
+            if (e == hipSuccess) e = hipEventRecord(h->cpy_ev, h->cpy);
+            if (e != hipSuccess) { hip_fail(h, e, "H2D R"); return nullptr; }
+            return h->cpy_ev;
+        };
+    } else {
+        HIP_TRY(hipMemcpy2DAsync(ws + l.inR, W, R, stride, W, H, hipMemcpyHostToDevice, st), "H2D R");
+    }
+    rc = run_pipeline(h, l, g, (const uint8_t*)(ws + l.inL), (const uint8_t*)(ws + l.inR), W, d16, W, copy_r, outf,
+                      out_stride);
     if (rc) return rc;
+    if (outf) {
+        HIP_TRY(hipStreamSynchronize(st), "sync");
+        return mark_done(h, st);
+    }
     const void* dsrc = d16;
     if (f32) {
         HIP_TRY(sgm::launch_to_f32(d16, W, (float*)(ws + l.outf), W, W, H, st), "to_f32");
@@ -917,6 +984,9 @@ void sgm_destroy(sgm_handle* h)
         for (hipEvent_t e : h->io_ev) (void)hipEventDestroy(e);
         if (h->io_dev) (void)hipFree(h->io_dev);
         if (h->io_pin) (void)hipHostFree(h->io_pin);
+        if (h->cpy) { (void)hipStreamSynchronize(h->cpy); (void)hipStreamDestroy(h->cpy); }
+        if (h->cpy_ev) (void)hipEventDestroy(h->cpy_ev);
+        for (const auto& r : h->regs) (void)hipHostUnregister(r.host);
         if (h->done) (void)hipEventDestroy(h->done);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
@@ -947,11 +1017,16 @@ int sgm_host_register(sgm_handle* h, void* ptr, size_t bytes)
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
     // a failed registration is not fatal to the caller (it falls back to pageable copies), so
     // HIP's last error is cleared here: the next launcher's hipGetLastError must not report it
-    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return hip_fail(h, e, "hipHostRegister");
     }
+    void* dev = nullptr;
+    if ((e = hipHostGetDevicePointer(&dev, ptr, 0)) != hipSuccess) dev = nullptr;   // registered, not mapped
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->regs.push_back({(char*)ptr, bytes, (char*)dev});
     return SGM_OK;
 }
 
@@ -960,6 +1035,12 @@ int sgm_host_unregister(sgm_handle* h, void* ptr)
     if (!h) return SGM_ERR_ARG;
     if (!ptr) return fail(h, SGM_ERR_ARG, "null host pointer");
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (h->done_stream) HIP_TRY(hipEventSynchronize(h->done), "hipEventSynchronize");   // no kernel still writes it
+        for (size_t i = 0; i < h->regs.size(); i++)
+            if (h->regs[i].host == (char*)ptr) { h->regs.erase(h->regs.begin() + i); break; }
+    }
     const hipError_t e = hipHostUnregister(ptr);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -1432,8 +1513,8 @@ int ensure_io(sgm_handle* h, size_t WH)
     // workgroups are dispatched ahead of the pipeline launch's queued ones
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-    const char* pe = std::getenv("SGM_IO_PRIO");
-    const int prio = (pe && std::atoi(pe) == 0) ? 0 : hi;
+    // (-DSGM_IO_PRIO=0, a measurement build: the copy streams at the default priority)
+    const int prio = SGM_IO_PRIO ? hi : 0;
     if (!h->up) HIP_TRY(hipStreamCreateWithPriority(&h->up, hipStreamNonBlocking, prio), "hipStreamCreate");
     if (!h->down) HIP_TRY(hipStreamCreateWithPriority(&h->down, hipStreamNonBlocking, prio), "hipStreamCreate");
     while (h->io_ev.size() < 3 * kIoRing + 1) {
@@ -1591,16 +1672,20 @@ static void enable_peer_pair(int a, int b);
 static int tiled_copy(void* dst, int ddev, size_t dpitch, const void* src, int sdev, size_t spitch, size_t width,
                       size_t rows, hipStream_t st)
 {
-    if (ddev == sdev || (dpitch == width && spitch == width)) {
-        const hipError_t e = ddev == sdev ? hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows,
-                                                             hipMemcpyDeviceToDevice, st)
-                                          : hipMemcpyPeerAsync(dst, ddev, src, sdev, width * rows, st);
+    if (ddev != sdev && dpitch == width && spitch == width) {      // contiguous rows: one peer copy
+        const hipError_t e = hipMemcpyPeerAsync(dst, ddev, src, sdev, width * rows, st);
         return e == hipSuccess ? 0 : (int)e;
     }
-    for (size_t r = 0; r < rows; r++) {       // strided rows across devices: one peer copy per row
-        const hipError_t e = hipMemcpyPeerAsync((char*)dst + r * dpitch, ddev, (const char*)src + r * spitch, sdev,
-                                                width, st);
-        if (e != hipSuccess) return (int)e;
+    // strided rows (or one device): one 2-D copy over the unified address space, the same call
+    // within a device and between peers (the launcher enabled peer access between the pair)
+    const hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDefault, st);
+    if (e == hipSuccess) return 0;
+    if (ddev == sdev) return (int)e;
+    (void)hipGetLastError();
+    for (size_t r = 0; r < rows; r++) {       // a runtime that refuses the peer 2-D copy: one copy per row
+        const hipError_t e2 = hipMemcpyPeerAsync((char*)dst + r * dpitch, ddev, (const char*)src + r * spitch, sdev,
+                                                 width, st);
+        if (e2 != hipSuccess) return (int)e2;
     }
     return 0;
 }

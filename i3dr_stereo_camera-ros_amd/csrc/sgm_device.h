@@ -242,9 +242,11 @@ __device__ __forceinline__ void wta_batch(const int (&S)[U][DPL], int lane, cons
 //  2. LR check: invalid iff both rounded candidates are in range, have disp2 >= minD and
 //     differ by more than disp12.
 //  3. store of the full row (columns outside [minX1, maxX1) stay invalid).
-// `key` needs W uint32; `d2` may alias `mins` (mins is dead after step 1).
+// `key` needs W uint32; `d2` may alias `mins` (mins is dead after step 1). OutT = float: the
+// row goes out as the node's CV_32FC1 (every int16 is exact in float).
+template <typename OutT>
 __device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, const int16_t* drow, const int16_t* bst,
-                                           const uint16_t* mins, uint32_t* key, int16_t* d2, int16_t* orow)
+                                           const uint16_t* mins, uint32_t* key, int16_t* d2, OutT* orow)
 {
     __syncthreads();
     for (int x = g.minX1 + tid; x < g.maxX1; x += nthr) {
@@ -270,7 +272,7 @@ __device__ __forceinline__ void row_finish(const Geom& g, int tid, int nthr, con
                 0 <= x_ && x_ < g.W && d2[x_] >= g.minD && abs(d2[x_] - d_) > g.disp12)
                 d1 = g.invalid;
         }
-        orow[x] = (int16_t)d1;
+        orow[x] = (OutT)d1;
     }
 }
 
@@ -290,6 +292,11 @@ struct WtaFrames {
     const uint8_t* vols[kMaxGroup];
     int16_t* out[kMaxGroup];
     int n;
+    // the standalone WTA launch only: when outf[0] is set, the rows go out as float (CV_32FC1)
+    // to outf (a host buffer mapped into the device's address space, sgm_host_register) instead
+    // of int16 to out, with this row stride in floats
+    float* outf[kMaxGroup];
+    size_t outf_stride;
     // up+WTA blocks (census_sgm.hip UpWta): the frames' codes and per-pixel result images
     const uint64_t* cL[kMaxGroup];
     const uint64_t* cR[kMaxGroup];

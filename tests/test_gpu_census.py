@@ -289,11 +289,13 @@ def test_c5_tiled_vs_full_frame(engine, synth, pkg):
     assert (full != -16).mean() > 0.5
 
 
-@pytest.mark.parametrize("bands,halo,n_dev,pad", [(1, 0, 1, 0), (3, 16, 2, 0), (4, 64, 4, 13), (5, 200, 3, 7)])
+@pytest.mark.parametrize("bands,halo,n_dev,pad", [(1, 0, 1, 0), (3, 16, 2, 0), (4, 64, 4, 13), (5, 200, 3, 7),
+                                                    (2, 32, 2, 9)])
 def test_tiled_device_equals_host_tiles(engine, oracle, synth, pkg, bands, halo, n_dev, pad):
     """sgm_match_tiled_device (device buffers, band b on devices[b % n], here all device 0 as
     bench.py --config c5 runs it with N bands on one GPU) is band for band the oracle on the
-    band's extended rows, i.e. the host overlap mode; strided input / output rows included."""
+    band's extended rows, i.e. the host overlap mode; strided input / output rows included (one
+    2-D copy per band and direction, the call the cross-device bands make too)."""
     import torch
     h, w, D = 200, 320, 96
     left, right, _ = synth.stereo_pair(h, w, 0, D, seed=47 + bands)
@@ -393,14 +395,16 @@ def test_c5_tiled_exact_vs_full_frame(engine, synth, pkg):
     assert np.array_equal(tiled, full), f"{(tiled != full).sum()} pixels differ"
 
 
+@pytest.mark.parametrize("D", [64, 48])
 @pytest.mark.parametrize("kw", [dict(), dict(speckle_window_size=30, speckle_range=2), dict(median=1)])
 @pytest.mark.parametrize("f32", [False, True])
-def test_registered_output_copy_out(engine, oracle, synth, pkg, kw, f32):
-    """sgm_host_register'ed outputs (the adapter's persistent disparity_lr, copied back by DMA
-    without pageable staging): same result as the oracle and as an unregistered output, with
-    and without post filters, in sgm_match (int16) and sgm_match_f32, the registration reused
-    across calls."""
-    h, w, D = 203, 300, 64
+def test_registered_output_copy_out(engine, oracle, synth, pkg, kw, f32, D):
+    """sgm_host_register'ed outputs (the adapter's persistent disparity_lr, page-locked and mapped):
+    same result as the oracle and as an unregistered output, with and without post filters, in
+    sgm_match (int16, copied back by DMA) and sgm_match_f32 (without post filters the WTA writes
+    the float rows straight into the mapped buffer, k_census_wta16f), the registration reused
+    across calls; the right image's copy overlaps the left census (second stream)."""
+    h, w = 203, 300
     left, right, _ = synth.stereo_pair(h, w, 0, D, seed=77)
     p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D, **kw)
     engine.set_params(p)
