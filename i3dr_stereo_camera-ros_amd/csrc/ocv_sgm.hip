@@ -502,6 +502,12 @@ template <int R, int DPC, int I>
 #ifndef SGM_FUSE_NB_WIDE
 #define SGM_FUSE_NB_WIDE 256     // A/B: box threads for R > 9 (512: every wave)
 #endif
+#ifndef SGM_FUSE_RKOFF
+#define SGM_FUSE_RKOFF 1         // the right-entry LDS base kept opaque (read2 immediates, no add per read)
+#endif
+#ifndef SGM_FUSE_BUFST
+#define SGM_FUSE_BUFST 1         // C' stores through a row descriptor (scalar offsets, no per-store VALU)
+#endif
 #ifndef SGM_FUSE_WPE
 #define SGM_FUSE_WPE -1          // waves per SIMD asked of the compiler (4: <= 128 VGPRs); -1: 4 for R > 9
 #endif
@@ -577,6 +583,11 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     // registers, slot v mod R picked by a uniform switch (static register indices, one copy of
     // the row code)
     const int kc = t / TPC, tq = t % TPC;
+    // the thread's first right-entry word of staging buffer 0 (loop-invariant, kept opaque so the
+    // per-row reads are one base add + ds_read2 immediates, not one add per read: the folded
+    // 6*NX*4-byte constant had pushed every read2 offset out of its 1020-byte range)
+    int rk_off = 6 * NX + 7 * (((M - DC - kc + 2 * tq * I) & 1) * MH + ((M - DC - kc + 2 * tq * I) >> 1));
+    if constexpr (SGM_FUSE_RKOFF != 0) asm volatile("" : "+v"(rk_off));
     // kRing8: a pixel cost is <= 2*ftzero + 63 <= 255 (the launcher's condition), so the ring
     // keeps bytes, two disparity pairs per register
     constexpr bool kRing8 = SGM_FUSE_RING8 != 0;
@@ -645,8 +656,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             u16x2_t u[2], ulo[2], uhi[2];
 #pragma unroll
             for (int c = 0; c < 2; c++) { u[c] = wd(Lk, 3 * c); ulo[c] = wd(Lk, 3 * c + 1); uhi[c] = wd(Lk, 3 * c + 2); }
-            const int j0 = M - DC - kc + 2 * tq * I;
-            const uint32_t* Rk = S + 6 * NX + 7 * ((j0 & 1) * MH + (j0 >> 1));
+            const uint32_t* Rk = S + rk_off;
             uint32_t P[I];
 #pragma unroll
             for (int q = 0; q < I; q++) {
@@ -713,14 +723,23 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
 #pragma unroll
             for (int i = 1; i < R; i++) sum += w[i];
             // 32-bit element offsets off the uniform C' base (C' < 2^32 words: the launcher's
-            // condition): one register per store instead of a 64-bit address
+            // condition)
             const uint32_t ob = (uint32_t)y * (uint32_t)rowC + (uint32_t)(((x0 + xa) * gD + d0) / 2 + bp);
+            // stores through a descriptor of the row (wave-uniform base, SGPRs): the lane's byte
+            // offset in one VGPR and output j's step as the scalar offset, no per-store VALU
+            const __amdgpu_buffer_rsrc_t crow = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(C32 + (size_t)y * rowC), 0, (int)(rowC * 4), 0x00020000);
+            const uint32_t vb = 4u * (uint32_t)(((x0 + xa) * gD + d0) / 2 + bp);
 #pragma unroll
             for (int j = 0; j < L; j++) {
                 if (j > 0) sum += w[j + R - 1] - w[j - 1];
                 if (xa + j < xb) {
                     if (!(col0 && xa + j == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
-                    C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum + p2v);
+                    if constexpr (SGM_FUSE_BUFST != 0)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum + p2v), crow, (int)vb,
+                                                              j * gD * 2, 0);
+                    else
+                        C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum + p2v);
                 }
             }
             if (tail) {                                      // OpenCV's bottom rows: never recomputed

@@ -39,6 +39,9 @@ hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
+#ifdef SGM_EXPERIMENT_BUILD
+hipError_t launch_strip3_proto(const uint64_t*, const uint64_t*, const Geom&, int, int, uint32_t*, uint32_t*, hipStream_t);
+#endif
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -2271,3 +2274,67 @@ int sgm_debug_speckle(sgm_handle* h, int16_t* disp, int W, int H, int new_val, i
 }
 
 }  // extern "C"
+
+#ifdef SGM_EXPERIMENT_BUILD
+// DESIGN §8.2 prototype A/B (experiment builds only, tools/strip3_ab.py): on the census codes of
+// one frame (h's census parameters), ms per launch averaged over `reps`, interleaved:
+// ms[0] the three top-down directions (0, 2, 3) of k_census_paths16 (three u8 volumes),
+// ms[1] k_strip3_proto with strips of ncol - 2G columns (one u16 partial-sum volume),
+// ms[2] all eight directions of k_census_paths16 (the single-frame paths launch).
+extern "C" int sgm_exp_strip3(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, int H, int ncol, int G,
+                              int reps, float* ms)
+{
+    if (!h || !ms || h->params.mode != SGM_MODE_CENSUS8) return SGM_ERR_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    Geom g;
+    Layout l;
+    int rc = prepare(h, W, H, false, g, l);
+    if (rc || (rc = order_after_last(h, h->stream))) return rc;
+    hipStream_t st = h->stream;
+    char* ws = (char*)h->ws.base;
+    uint64_t* cL = (uint64_t*)(ws + l.cL[0]);
+    uint64_t* cR = (uint64_t*)(ws + l.cR[0]);
+    uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
+    HIP_TRY(sgm::launch_census(dL, dR, W, W, H, cL, cR, st), "census");
+    const uint32_t *it_down, *it_all;
+    const int n_down = path_items(h, l, g, 0x0Du, 1, st, &it_down);
+    if (n_down < 0) return n_down;
+    std::vector<uint32_t> down_copy(n_down);
+    HIP_TRY(hipMemcpyAsync(down_copy.data(), it_down, (size_t)n_down * 4, hipMemcpyDeviceToHost, st), "items");
+    HIP_TRY(hipStreamSynchronize(st), "sync");
+    uint32_t* items_down = nullptr;
+    HIP_TRY(hipMalloc(&items_down, (size_t)n_down * 4), "hipMalloc");
+    HIP_TRY(hipMemcpy(items_down, down_copy.data(), (size_t)n_down * 4, hipMemcpyHostToDevice), "items");
+    const int n_all = path_items(h, l, g, 0xFFu, 1, st, &it_all);
+    if (n_all < 0) return n_all;
+    const int strips = (g.width1 + (ncol - 2 * G) - 1) / std::max(ncol - 2 * G, 1);
+    uint32_t* edge = nullptr;
+    HIP_TRY(hipMalloc(&edge, (size_t)strips * 2 * (g.D / 32) * 16 * std::max(G, 1) * 4 + 4096), "hipMalloc");
+    uint32_t* S3 = (uint32_t*)(vols + 4 * l.vol_bytes);           // direction slots 4-5: unused here
+    sgm::PathFrames pf{};
+    pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
+    hipEvent_t e[2];
+    HIP_TRY(hipEventCreate(&e[0]), "ev");
+    HIP_TRY(hipEventCreate(&e[1]), "ev");
+    double acc[3] = {0, 0, 0};
+    for (int r = -1; r < reps; r++) {
+        for (int k = 0; k < 3; k++) {
+            HIP_TRY(hipEventRecord(e[0], st), "ev");
+            if (k == 0) HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items_down, n_down, st), "down");
+            else if (k == 1) HIP_TRY(sgm::launch_strip3_proto(cL, cR, g, ncol, G, S3, edge, st), "strip3");
+            else HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, it_all, n_all, st), "all");
+            HIP_TRY(hipEventRecord(e[1], st), "ev");
+            HIP_TRY(hipEventSynchronize(e[1]), "sync");
+            float t = 0;
+            HIP_TRY(hipEventElapsedTime(&t, e[0], e[1]), "elapsed");
+            if (r >= 0) acc[k] += t;
+        }
+    }
+    for (int k = 0; k < 3; k++) ms[k] = (float)(acc[k] / std::max(reps, 1));
+    (void)hipEventDestroy(e[0]);
+    (void)hipEventDestroy(e[1]);
+    (void)hipFree(edge);
+    (void)hipFree(items_down);
+    return mark_done(h, st);
+}
+#endif
