@@ -1118,6 +1118,68 @@ __device__ __forceinline__ int line_min_i32(int v)
 // buffer offset of a dropped store: past every buffer range the buffer path is used for
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
+#ifndef SGM_OCV_PK
+#define SGM_OCV_PK 1       // the plain int16 path recurrence in packed u16 pairs (0: one int per value)
+#endif
+// The plain (non-SAT) int16 regime of the path recurrence in packed u16 pairs. There every
+// C' lies in [P2, 32767] (box sum + P2, no cost left int16: the gate's condition), so with
+// delta = minLp + P2 the candidates Lp, Lp(d -+ 1) + P1 and delta stay below 65536 (P1, P2 <=
+// 32768: the launcher's condition) and OpenCV's C + min(...) - delta = C - (delta - min(...))
+// never leaves [0, 32767]: the u16 halves are exactly OpenCV's int values and its CostType
+// copies. A lane's DPL values are DPL / 2 dwords as loaded from C' and stored to the volume
+// (no unpacking), the neighbours two alignbits of adjacent pairs and one DPP per lane edge.
+template <int LPL>
+__device__ __forceinline__ uint32_t line_shr1_u(uint32_t v, int p)      // lane p <- p - 1; line start: 0xFFFFFFFF
+{
+    if constexpr (LPL == 16) return row_shr1(v, 0xFFFFFFFFu);
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x138, 0xf, 0xf, false);
+    return (LPL == 64 || p != 0) ? t : 0xFFFFFFFFu;
+}
+template <int LPL>
+__device__ __forceinline__ uint32_t line_shl1_u(uint32_t v, int p)      // lane p <- p + 1; line end: 0xFFFFFFFF
+{
+    if constexpr (LPL == 16) return row_shl1(v, 0xFFFFFFFFu);
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)v, 0x130, 0xf, 0xf, false);
+    return (LPL == 64 || p != LPL - 1) ? t : 0xFFFFFFFFu;
+}
+// One step: L2 (the previous L of the lane's pairs) -> the new L; returns the lane's min over
+// its valid d (entries with d >= D are forced to kMaxCost = 32767 by imask, as OpenCV pads).
+template <int DPL, int LPL>
+__device__ __forceinline__ uint32_t ocv_step_pk(const uint32_t (&C2)[DPL / 2], uint32_t (&L2)[DPL / 2], uint32_t delta2,
+                                                uint32_t P1P1, const uint32_t (&imask)[DPL / 2], int p)
+{
+    constexpr int M = DPL / 2;
+    uint32_t q[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) q[i] = pk_add(L2[i], P1P1);
+    const uint32_t X = line_shr1_u<LPL>(q[M - 1], p), Y = line_shl1_u<LPL>(q[0], p);
+    uint32_t Op = alignbit16(q[0], X);                   // (q(d - 1), q(d)) of pair 0
+    uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        const uint32_t On = (i + 1 < M) ? alignbit16(q[i + 1], q[i]) : alignbit16(Y, q[M - 1]);
+        const uint32_t t = pk_min(pk_min(Op, On), pk_min(L2[i], delta2));
+        const uint32_t v = pk_sub(C2[i], pk_sub(delta2, t));
+        L2[i] = (v & ~imask[i]) | (0x7FFF7FFFu & imask[i]);
+        mn = pk_min(mn, L2[i]);
+        Op = On;
+    }
+    return min(mn & 0xFFFFu, mn >> 16);
+}
+template <int N>
+__device__ __forceinline__ void bload_dw(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t (&w)[N])
+{
+    if constexpr (N == 1) w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+    else if constexpr (N == 2) { const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0); w[0] = t[0]; w[1] = t[1]; }
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 4; c++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * c, 0, 0);
+            w[4 * c] = t[0]; w[4 * c + 1] = t[1]; w[4 * c + 2] = t[2]; w[4 * c + 3] = t[3];
+        }
+    }
+}
+
 // 64 / LPL path lines per wave. Block b of direction dir holds its lines NLW*b .. NLW*b +
 // NLW - 1: horizontal (ry == 0) line = row; row sweeps (ry != 0): lines [0, width1) start on
 // the first row at that column, the others on the entry column at row offset
@@ -1127,7 +1189,7 @@ constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 template <int DPL, int LPL, typename VT, bool SAT>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, VT* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
-                                                  int4 nblk1, int use_buf)
+                                                  int4 nblk1, int use_buf, int use_pk)
 {
     if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
@@ -1183,6 +1245,51 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     const int dl = lane_act ? p * DPL : g.D - DPL;
     // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop).
     // The first PF steps are peeled (pv = false only at step 0, a constant elsewhere).
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 2) {
+        if (use_buf && use_pk) {     // the plain int16 regime in packed u16 pairs (ocv_step_pk)
+            constexpr int M = DPL / 2;
+            const size_t cells = (size_t)g.width1 * g.H * g.D;
+            const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(uint32_t)(cells * 2), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc((void*)V, 0, (int)(uint32_t)(cells * 2), 0x00020000);
+            const uint32_t bstep = (uint32_t)(cstep * 2);
+            uint32_t ld_b = (uint32_t)((cbase + dl) * 2), st_b = ld_b;
+            uint32_t imask[M];
+#pragma unroll
+            for (int i = 0; i < M; i++)
+                imask[i] = (p * DPL + 2 * i < g.D ? 0u : 0xFFFFu) | (p * DPL + 2 * i + 1 < g.D ? 0u : 0xFFFF0000u);
+            const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2 = (uint32_t)g.P2;
+            uint32_t C2[PF][M], L2[M];
+#pragma unroll
+            for (int i = 0; i < M; i++) L2[i] = 0;
+            uint32_t delta2 = P2 * 0x10001u;             // the path's first pixel: L = C - P2
+#pragma unroll
+            for (int q = 0; q < PF; q++) { bload_dw<M>(rsC, ld_b, C2[q]); ld_b += bstep; }
+            auto steps = [&](int i0) {
+#pragma unroll
+                for (int q = 0; q < PF; q++) {
+                    const int i = i0 + q;
+                    const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2[q], L2, delta2, P1P1, imask, p);
+                    const bool ok = lane_act && i < n;
+                    if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
+                        bstore_dw<8>(rsV, ok ? st_b : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
+                        bstore_dw<8>(rsV, ok && !straddle ? st_b + 32u : kBufDrop,
+                                     *reinterpret_cast<const uint32_t(*)[8]>(&L2[8]));
+                    } else {
+                        bstore_dw<M>(rsV, ok ? st_b : kBufDrop, L2);
+                    }
+                    delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
+                    bload_dw<M>(rsC, ld_b, C2[q]);
+                    st_b += bstep;
+                    ld_b += bstep;
+                }
+            };
+            for (int i0 = 0; i0 < nmax; i0 += PF) {
+                if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+                steps(i0);
+            }
+            return;
+        }
+    }
     if (use_buf) {
         // Volumes < 4 GB - 256 B: raw buffer loads and stores with 32-bit byte offsets that just
         // move by the step (mod 2^32); a step past the line's end reads whatever lies there
@@ -1775,9 +1882,11 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
     // 32-bit buffer offsets when a volume ends below kBufDrop (the shipped 2448x2048 D=480
     // config's int16 volumes are 3.6 GB; SGM_OCV_NO_BUF=1 forces the 64-bit path)
     const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < (size_t)kBufDrop && !getenv("SGM_OCV_NO_BUF");
+    // packed u16 recurrence: the plain int16 regime with P1, P2 <= 32768 (SGM_OCV_PK=0 at build time: ints)
+    const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
     if (total > 0)
         hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
-                       dirmask, a, b, use_buf);
+                       dirmask, a, b, use_buf, use_pk);
 }
 
 // the plain kernels (wide != 1) and the flagged ones (wide != 0): int32 volumes for the scalar

@@ -109,10 +109,12 @@ int  sgm_device_count(void);
 int  sgm_create(sgm_handle** out, int device);
 void sgm_destroy(sgm_handle* h);
 
-/* Page-lock a caller's host buffer (hipHostRegister) for as long as it stays registered: a
- * registered output of sgm_match / sgm_match_f32 is copied back by DMA without the runtime's
- * pageable staging. The caller must unregister a buffer before freeing it (the MatcherHIPSGM
- * adapter registers its persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat).      */
+/* Page-lock and map a caller's host buffer (hipHostRegister, mapped) for as long as it stays
+ * registered: a registered output of sgm_match / sgm_match_f32 is copied back by DMA without the
+ * runtime's pageable staging, or — sgm_match_f32 in the census mode without median / speckles —
+ * written by the WTA kernel itself as the rows finish. The caller must unregister a buffer
+ * before freeing it (unregistering waits for the handle's last call); the MatcherHIPSGM adapter
+ * registers its persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat.               */
 int  sgm_host_register(sgm_handle* h, void* ptr, size_t bytes);
 int  sgm_host_unregister(sgm_handle* h, void* ptr);
 
