@@ -1562,7 +1562,7 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
 // on tall frames with many columns (the shipped 2448x2048 config), not on small ones.
 template <int DPL, int NDIR, typename VT, bool SAT>
 __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, const VT* __restrict__ vols,
-                                                 size_t vol_elems, Geom g, uint64_t* __restrict__ res)
+                                                 size_t vol_elems, Geom g, uint64_t* __restrict__ res, int use_pk)
 {
     if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
     constexpr int LPL = 64;                            // one column per wave: the line is the wave
@@ -1591,19 +1591,47 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
     int Lp[DPL], mLp = 0, Cq[PF][DPL], Vq[PF][NDIR][DPL];
 #pragma unroll
     for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
+    // the plain int16 regime: the recurrence in packed u16 pairs (ocv_step_pk), the WTA on ints
+    constexpr bool kPk = !SAT && sizeof(VT) == 2 && DPL >= 2 && SGM_OCV_PK != 0;
+    constexpr int M2 = DPL >= 2 ? DPL / 2 : 1;
+    uint32_t L2[M2], imask2[M2], delta2 = (uint32_t)g.P2 * 0x10001u;
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u;
+#pragma unroll
+    for (int i = 0; i < M2; i++) {
+        L2[i] = 0;
+        imask2[i] = (p * DPL + 2 * i < g.D ? 0u : 0xFFFFu) | (p * DPL + 2 * i + 1 < g.D ? 0u : 0xFFFF0000u);
+    }
 #pragma unroll
     for (int q = 0; q < PF; q++) load(q, Cq[q], Vq[q]);
     // step i: the recurrence (a chain through mLp), then the pixel's WTA, which no later step
     // waits for: S[best +- 1] come from a readlane (best is wave-uniform), so no LDS barrier
     // orders the steps and the WTA of one step overlaps the recurrence of the next
     auto step = [&](int i, int (&Cc)[DPL], int (&V)[NDIR][DPL]) {
-        int L[DPL], Lraw[DPL];
-        const int lmin = ocv_step<DPL, LPL, SAT>(Cc, Lp, mLp, i > 0, p, g, L, Lraw);
-        mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
+        bool done = false;
+        if constexpr (kPk) {
+            if (use_pk) {                              // (the path's first pixel: L2 = 0, delta = P2)
+                uint32_t C2[M2];
 #pragma unroll
-        for (int k = 0; k < DPL; k++) {
-            Lp[k] = L[k];
-            V[F][k] = kRaw ? Lraw[k] : L[k];           // what the volume would have held
+                for (int j = 0; j < M2; j++) C2[j] = ((uint32_t)Cc[2 * j] & 0xFFFFu) | ((uint32_t)Cc[2 * j + 1] << 16);
+                const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2, L2, delta2, P1P1, imask2, p);
+                delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + (uint32_t)g.P2) * 0x10001u;
+#pragma unroll
+                for (int j = 0; j < M2; j++) {
+                    V[F][2 * j] = (int)(L2[j] & 0xFFFFu);
+                    V[F][2 * j + 1] = (int)(L2[j] >> 16);
+                }
+                done = true;
+            }
+        }
+        if (!done) {
+            int L[DPL], Lraw[DPL];
+            const int lmin = ocv_step<DPL, LPL, SAT>(Cc, Lp, mLp, i > 0, p, g, L, Lraw);
+            mLp = (int)(int16_t)line_min_i32<LPL>(lmin);   // minLr is CostType
+#pragma unroll
+            for (int k = 0; k < DPL; k++) {
+                Lp[k] = L[k];
+                V[F][k] = kRaw ? Lraw[k] : L[k];           // what the volume would have held
+            }
         }
         int S[DPL];
         int km = 0x7FFFFFFF;                           // keys < 2^27: signed min
@@ -2003,8 +2031,9 @@ static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, 
                               hipStream_t st)
 {
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
+    const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
     hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols, vol_elems,
-                       g, res);
+                       g, res, use_pk);
 }
 template <int DPL, int NDIR>
 static void launch_ocv_vwta_v(const int16_t* C, const int16_t* Csat, const void* vols, size_t cells, const Geom& g,
