@@ -1119,7 +1119,7 @@ __device__ __forceinline__ int line_min_i32(int v)
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
 #ifndef SGM_OCV_PK
-#define SGM_OCV_PK 1       // the plain int16 path recurrence in packed u16 pairs (0: one int per value)
+#define SGM_OCV_PK 0       // 1: the plain int16 path recurrence in packed u16 pairs (bit-exact; measured slower, profiles/r05_ocv_pk_cost_ab.jsonl)
 #endif
 // The plain (non-SAT) int16 regime of the path recurrence in packed u16 pairs. There every
 // C' lies in [P2, 32767] (box sum + P2, no cost left int16: the gate's condition), so with
