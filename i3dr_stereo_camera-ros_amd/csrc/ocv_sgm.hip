@@ -506,7 +506,9 @@ template <int R, int DPC, int I>
 #define SGM_FUSE_RKOFF 1         // the right-entry LDS base kept opaque (read2 immediates, no add per read)
 #endif
 #ifndef SGM_FUSE_BUFST
-#define SGM_FUSE_BUFST 1         // C' stores through a row descriptor (scalar offsets, no per-store VALU)
+#define SGM_FUSE_BUFST 9         // C' stores through a row descriptor (scalar offsets, no per-store VALU) for
+                                 // boxes up to this size (1080p block 5: 0.221 -> 0.217 ms; the shipped
+                                 // block 21: 2.00 -> 2.05 ms, so not there; profiles/r05_ocv_pk_cost_ab.jsonl)
 #endif
 #ifndef SGM_FUSE_WPE
 #define SGM_FUSE_WPE -1          // waves per SIMD asked of the compiler (4: <= 128 VGPRs); -1: 4 for R > 9
@@ -735,7 +737,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 if (j > 0) sum += w[j + R - 1] - w[j - 1];
                 if (xa + j < xb) {
                     if (!(col0 && xa + j == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
-                    if constexpr (SGM_FUSE_BUFST != 0)
+                    if constexpr (R <= SGM_FUSE_BUFST)
                         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum + p2v), crow, (int)vb,
                                                               j * gD * 2, 0);
                     else
