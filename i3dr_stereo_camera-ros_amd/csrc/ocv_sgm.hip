@@ -1120,6 +1120,9 @@ __device__ __forceinline__ int line_min_i32(int v)
 // buffer offset of a dropped store: past every buffer range the buffer path is used for
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
+#ifndef SGM_OCV_PK_PF
+#define SGM_OCV_PK_PF 8    // packed path lines: cost rows in flight (up to 4 dwords per lane; half above)
+#endif
 #ifndef SGM_OCV_PK
 #define SGM_OCV_PK 0       // 1: the plain int16 path recurrence in packed u16 pairs (bit-exact; measured slower, profiles/r05_ocv_pk_cost_ab.jsonl)
 #endif
@@ -1260,6 +1263,9 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             for (int i = 0; i < M; i++)
                 imask[i] = (p * DPL + 2 * i < g.D ? 0u : 0xFFFFu) | (p * DPL + 2 * i + 1 < g.D ? 0u : 0xFFFF0000u);
             const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2 = (uint32_t)g.P2;
+            // rows in flight: hipcc waits for all of an iteration's loads at its top (vmcnt(0)), so
+            // the iteration is PK_PF steps long: one memory latency per PK_PF steps
+            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? SGM_OCV_PK_PF / 2 : 2;
             uint32_t C2[PF][M], L2[M];
 #pragma unroll
             for (int i = 0; i < M; i++) L2[i] = 0;
