@@ -1121,10 +1121,10 @@ __device__ __forceinline__ int line_min_i32(int v)
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
 #ifndef SGM_OCV_PK_PF
-#define SGM_OCV_PK_PF 8    // packed path lines: cost rows in flight (up to 4 dwords per lane; half above)
+#define SGM_OCV_PK_PF 16   // packed path lines: cost rows in flight for up to 4 dwords per lane (4 for 8, 2 for 16)
 #endif
 #ifndef SGM_OCV_PK
-#define SGM_OCV_PK 0       // 1: the plain int16 path recurrence in packed u16 pairs (bit-exact; measured slower, profiles/r05_ocv_pk_cost_ab.jsonl)
+#define SGM_OCV_PK 1       // the plain int16 path recurrence in packed u16 pairs (0: one int per value)
 #endif
 // The plain (non-SAT) int16 regime of the path recurrence in packed u16 pairs. There every
 // C' lies in [P2, 32767] (box sum + P2, no cost left int16: the gate's condition), so with
@@ -1265,7 +1265,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2 = (uint32_t)g.P2;
             // rows in flight: hipcc waits for all of an iteration's loads at its top (vmcnt(0)), so
             // the iteration is PK_PF steps long: one memory latency per PK_PF steps
-            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? SGM_OCV_PK_PF / 2 : 2;
+            // (1080p D=128 MODE_SGBM paths, M = 4: 0.97 ms unpacked, packed 0.91 / 0.86 / 0.84 at 4 / 8 /
+            // 16 rows; the shipped D=480 config, M = 8: 6.20 ms unpacked and at 4 rows, 6.79 at 8;
+            // profiles/r05_ocv_pk_ab.jsonl)
+            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? 4 : 2;
             uint32_t C2[PF][M], L2[M];
 #pragma unroll
             for (int i = 0; i < M; i++) L2[i] = 0;
@@ -1600,7 +1603,9 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
 #pragma unroll
     for (int k = 0; k < DPL; k++) Lp[k] = kMaxCost;
     // the plain int16 regime: the recurrence in packed u16 pairs (ocv_step_pk), the WTA on ints
-    constexpr bool kPk = !SAT && sizeof(VT) == 2 && DPL >= 2 && SGM_OCV_PK != 0;
+    // (DPL >= 8 only: the shipped D=480 config 3.55 -> 3.48 ms, while 1080p D=128 MODE_HH, DPL = 2,
+    // measured 0.87 -> 0.93 ms; profiles/r05_ocv_pk_ab.jsonl)
+    constexpr bool kPk = !SAT && sizeof(VT) == 2 && DPL >= 8 && SGM_OCV_PK != 0;
     constexpr int M2 = DPL >= 2 ? DPL / 2 : 1;
     uint32_t L2[M2], imask2[M2], delta2 = (uint32_t)g.P2 * 0x10001u;
     const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u;
