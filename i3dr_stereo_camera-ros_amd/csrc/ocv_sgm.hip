@@ -1949,13 +1949,19 @@ static void launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols
 // the 16-lane step, fewer instructions per cell, wins (MI355X: C1 640x480 D=64 0.36 vs
 // 0.39-0.42 ms per frame; 1920x1080 D=128 3.24 vs 2.85 ms). SGM_OCV_LPL=16|32 forces one.
 constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lanes pay
+#ifndef SGM_OCV_LPL_MID
+#define SGM_OCV_LPL_MID 64                  // lanes per line for 256 < D <= 512 (32 or 64: the shipped D=480
+                                            // MODE_SGBM paths 5.96 -> 5.63 ms, MODE_HH 11.2 -> 10.0, profiles/r05_ocv_lpl64_ab.jsonl)
+#endif
 static int ocv_lanes_per_line(const Geom& g, int dirmask)
 {
     if (g.D <= 32) return 16;
     if (g.D > 512) return 64;       // a line per wave: 16 or 32 values per lane (D <= 2048)
-    if (g.D > 256) return 32;       // 16 lanes x DPL 32 would straddle D when D % 32 = 16, and
+    if (g.D > 256) return SGM_OCV_LPL_MID;   // 16 lanes x DPL 32 would straddle D when D % 32 = 16, and
                                     // its 32-value step is slower anyway (the shipped 2448x2048
-                                    // D=480 config, MODE_SGBM paths: 17.4 ms vs 8.8 ms)
+                                    // D=480 config, MODE_SGBM paths: 17.4 ms vs 8.8 ms); 64 lanes
+                                    // of 8 values beat 32 of 16 once the packed step keeps 16 rows
+                                    // in flight (5.63 vs 5.96 ms)
     if (const char* e = getenv("SGM_OCV_LPL")) return atoi(e) == 32 ? 32 : 16;
     int waves = 0;
     for (int i = 0; i < 8; i++)
@@ -1970,7 +1976,8 @@ hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, s
     const int D = g.D;
     const int lpl = ocv_lanes_per_line(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
     if (lpl == 64) {
-        if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        if (D <= 512) launch_ocv_paths_v<8, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
         else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
     } else if (lpl == 32) {
         if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
