@@ -1120,6 +1120,9 @@ __device__ __forceinline__ int line_min_i32(int v)
 // buffer offset of a dropped store: past every buffer range the buffer path is used for
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
+#ifndef SGM_OCV_VWTA_PK
+#define SGM_OCV_VWTA_PK 1  // k_ocv_vwta_pk for the plain int16 regime with uniqueness < 100
+#endif
 #ifndef SGM_OCV_PK_PF
 #define SGM_OCV_PK_PF 16   // packed path lines: cost rows in flight for up to 4 dwords per lane (4 for 8, 2 for 16)
 #endif
@@ -2044,6 +2047,156 @@ hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& 
     return hipGetLastError();
 }
 
+// k_ocv_vwta in packed u16 pairs for the plain int16 regime (the step of ocv_step_pk; no flagged
+// frame, uniqueness ratio < 100). Every path cost there lies in [0, 32767], so OpenCV's S =
+// sat16(sat16(s1) + s2) is min(sum, 32767) in any order: saturating packed i16 adds of the
+// loaded dwords. Entries with d >= D are forced to 0xFFFF after the sum, above every real S.
+// The WTA decisions are k_ocv_vwta's: best and minS from one 64-lane min over
+// S << 11 | tie(d) (first minimal d, or the 3.x lane rule); uniqueness as a count — the number
+// of d with S < T = ceil(minS * 100 / (100 - u)) over the line (packed saturating subtract, a
+// per-lane sum, one 64-lane reduction) against the count inside {best - 1, best, best + 1}
+// (from minS and the two neighbours the subpixel step reads anyway): a d outside the window
+// qualifies iff the first exceeds the second.
+template <int LPL>
+__device__ __forceinline__ int line_sum_i32(int v)
+{
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true);     // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true);     // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, true);    // row_ror:4
+    v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, true);    // row_ror:8
+    if constexpr (LPL >= 32) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = (int)sw[0] + (int)sw[1];
+    }
+    if constexpr (LPL == 64) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = (int)sw[0] + (int)sw[1];
+    }
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void load_dw(const int16_t* p, uint32_t (&w)[N])
+{
+    if constexpr (N == 1) w[0] = *(const uint32_t*)p;
+    else if constexpr (N == 2) { const uint2 t = *(const uint2*)p; w[0] = t.x; w[1] = t.y; }
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 4; c++) {
+            const uint4 t = ((const uint4*)p)[c];
+            w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
+        }
+    }
+}
+template <int DPL, int NDIR>
+__global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ C, const int16_t* __restrict__ vols,
+                                                    size_t vol_elems, Geom g, uint64_t* __restrict__ res)
+{
+    if (ocv_gate_skip<false>(g)) return;
+    constexpr int LPL = 64, M = DPL / 2;
+    constexpr int F = NDIR == 5 ? 0 : 1;               // the fused direction = its volume slot
+    constexpr int PF = M <= 2 ? 4 : NDIR == 5 ? 3 : 2;
+    const int p = threadIdx.x;
+    const int x1 = blockIdx.x;
+    const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
+    const bool lane_act = p * DPL < g.D;
+    const int dl = lane_act ? p * DPL : g.D - DPL;     // lanes past D load the last group
+    auto cell = [&](int i) -> size_t {
+        const int y = F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0);
+        return ((size_t)y * g.width1 + x1) * g.D + dl;
+    };
+    auto load = [&](int i, uint32_t (&c)[M], uint32_t (&v)[NDIR][M]) {
+        const size_t o = cell(i);
+        load_dw<M>(C + o, c);
+#pragma unroll
+        for (int s = 0; s < NDIR; s++)
+            if (s != F) load_dw<M>(vols + (size_t)s * vol_elems + o, v[s]);
+    };
+    uint32_t imask[M], tie[M][2];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const int d = p * DPL + 2 * j;
+        imask[j] = (d < g.D ? 0u : 0xFFFFu) | (d + 1 < g.D ? 0u : 0xFFFF0000u);
+        tie[j][0] = (uint32_t)wta_tie(d, lanetie, 11);
+        tie[j][1] = (uint32_t)wta_tie(d + 1, lanetie, 11);
+    }
+    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2 = (uint32_t)g.P2;
+    // uniqueness threshold divisor (u < 100: the launcher's condition)
+    const int kq = 100 - g.uniq;
+    uint32_t L2[M], delta2 = P2 * 0x10001u;            // the path's first pixel: L = C - P2
+#pragma unroll
+    for (int j = 0; j < M; j++) L2[j] = 0;
+    uint32_t Cq[PF][M], Vq[PF][NDIR][M];
+#pragma unroll
+    for (int q = 0; q < PF; q++) load(q, Cq[q], Vq[q]);
+    auto step = [&](int i, const uint32_t (&Cc)[M], const uint32_t (&V)[NDIR][M]) {
+        const uint32_t lmin = ocv_step_pk<DPL, LPL>(Cc, L2, delta2, P1P1, imask, p);
+        delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
+        uint32_t S2[M];
+        int km = 0x7FFFFFFF;
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            s16x2_t a = __builtin_bit_cast(s16x2_t, L2[j]);
+#pragma unroll
+            for (int s = 0; s < NDIR; s++)
+                if (s != F) a = __builtin_elementwise_add_sat(a, __builtin_bit_cast(s16x2_t, V[s][j]));
+            S2[j] = __builtin_bit_cast(uint32_t, a) | imask[j];
+            const int klo = (int)(((S2[j] & 0xFFFFu) << 11) | tie[j][0]);
+            const int khi = (int)(((S2[j] >> 16) << 11) | tie[j][1]);
+            km = min(km, min(klo, khi));
+        }
+        const int kmin = __builtin_amdgcn_readfirstlane(line_min_i32<LPL>(km));
+        const int best = wta_untie(kmin & 2047, lanetie, 11);
+        const int minS = kmin >> 11;
+        // S of d (wave-uniform): one readlane per register of the lane holding d, then a select
+        auto s_at = [&](int d) {
+            const int ln = d / DPL, k = d % DPL, jj = k >> 1;
+            uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)S2[0], ln);
+#pragma unroll
+            for (int j = 1; j < M; j++) {
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)S2[j], ln);
+                v = jj == j ? r : v;
+            }
+            return (int)((k & 1) ? v >> 16 : v & 0xFFFFu);
+        };
+        const int sm = s_at(max(best - 1, 0)), sp = s_at(min(best + 1, g.D - 1));
+        // uniqueness: S * kq < minS * 100 <=> S < T = ceil(minS * 100 / kq); T clamped to 32768
+        // (every real S is <= 32767, and d >= D holds 0xFFFF)
+        const int Mq = minS * 100;
+        const int T = min((Mq + kq - 1) / kq, 32768);
+        const uint32_t T2 = (uint32_t)T * 0x10001u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            const uint32_t t = as_u(__builtin_elementwise_sub_sat(as_v2(T2), as_v2(S2[j])));   // > 0 where S < T
+            acc = pk_add(acc, pk_min(t, 0x00010001u));
+        }
+        const int total = line_sum_i32<LPL>((int)((acc & 0xFFFFu) + (acc >> 16)));
+        const int inwin = (best >= 1 && sm < T ? 1 : 0) + (minS < T ? 1 : 0) + (best + 1 < g.D && sp < T ? 1 : 0);
+        const bool rej = __builtin_amdgcn_readfirstlane(total) > inwin || minS >= 32767;
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int d16 = best * 16 + (use ? tdiv_rcp((sm - sp) * 16 + den, 2 * den) : 0) + g.minD * 16;
+        const int y = F == 0 ? i : g.H - 1 - i;
+        const uint64_t v = (uint64_t)(uint16_t)(rej ? g.invalid : d16) |
+                           ((uint64_t)(uint16_t)(rej ? -1 : best) << 16) | ((uint64_t)(uint16_t)minS << 32);
+        if (p == 0 && i < g.H) __builtin_nontemporal_store(v, res + (size_t)y * g.W + g.minX1 + x1);
+    };
+    for (int i0 = 0; i0 < g.H; i0 += PF) {
+#pragma unroll
+        for (int q = 0; q < PF; q++) {
+            uint32_t Cc[M], V[NDIR][M];
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                Cc[j] = Cq[q][j];
+#pragma unroll
+                for (int s = 0; s < NDIR; s++) V[s][j] = Vq[q][s][j];
+            }
+            load(i0 + q + PF, Cq[q], Vq[q]);           // operands of step i + PF
+            step(i0 + q, Cc, V);
+        }
+    }
+}
+
 // Fused vertical path + WTA (k_ocv_vwta): one 64-lane line (a column) per wave, DPL = D / 64
 // rounded up to a power of two; the plain and the flagged kinds as for the paths.
 template <int DPL, int NDIR, typename VT, bool SAT>
@@ -2052,6 +2205,13 @@ static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, 
 {
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 2) {
+        if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0) {     // everything packed (k_ocv_vwta_pk)
+            hipLaunchKernelGGL((k_ocv_vwta_pk<DPL, NDIR>), dim3(g.width1), dim3(64), 0, st, C, (const int16_t*)vols,
+                               vol_elems, g, res);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols, vol_elems,
                        g, res, use_pk);
 }
