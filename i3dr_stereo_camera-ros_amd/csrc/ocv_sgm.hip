@@ -1123,6 +1123,9 @@ constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 #ifndef SGM_OCV_VWTA_PK
 #define SGM_OCV_VWTA_PK 1  // k_ocv_vwta_pk for the plain int16 regime with uniqueness < 100
 #endif
+#ifndef SGM_OCV_VWTA_PK_PF
+#define SGM_OCV_VWTA_PK_PF 0  // k_ocv_vwta_pk steps in flight (0: by shape)
+#endif
 #ifndef SGM_OCV_PK_PF
 #define SGM_OCV_PK_PF 16   // packed path lines: cost rows in flight for up to 4 dwords per lane (4 for 8, 2 for 16)
 #endif
@@ -2094,7 +2097,9 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
     if (ocv_gate_skip<false>(g)) return;
     constexpr int LPL = 64, M = DPL / 2;
     constexpr int F = NDIR == 5 ? 0 : 1;               // the fused direction = its volume slot
-    constexpr int PF = M <= 2 ? 4 : NDIR == 5 ? 3 : 2;
+    // steps in flight: a column is one latency-bound chain (width1 waves, ~2 per SIMD), and the
+    // packed operands are half the registers of k_ocv_vwta's ints
+    constexpr int PF = SGM_OCV_VWTA_PK_PF > 0 ? SGM_OCV_VWTA_PK_PF : 8;
     const int p = threadIdx.x;
     const int x1 = blockIdx.x;
     const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
@@ -2205,8 +2210,13 @@ static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, 
 {
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
-    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 2) {
-        if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0) {     // everything packed (k_ocv_vwta_pk)
+    // everything packed (k_ocv_vwta_pk) for MODE_HH at >= 8 values per lane: the shipped D=480
+    // config's fused kernel 5.67 -> 5.27 ms with 8 steps in flight; MODE_SGBM (3.47 vs 3.53-3.60)
+    // and 1080p MODE_HH (0.87 vs 0.90-0.94) keep k_ocv_vwta (profiles/r05_ocv_vwta_pk_ab.jsonl):
+    // the kernel streams its volumes near the read peak, and fewer instructions help only where
+    // the operands of more steps fit in flight
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 8 && NDIR == 8) {
+        if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0) {
             hipLaunchKernelGGL((k_ocv_vwta_pk<DPL, NDIR>), dim3(g.width1), dim3(64), 0, st, C, (const int16_t*)vols,
                                vol_elems, g, res);
             return;
