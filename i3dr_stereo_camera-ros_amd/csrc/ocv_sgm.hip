@@ -487,7 +487,9 @@ struct FuseGeo {
 struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
 };
-template <int R, int DPC, int I>
+// TRK: what the overflow flag tracks (ocv_fuse_track): 0 nothing (no gate), 1 the max of C' itself
+// (box + P2 below 2^16 whatever the pixels; P2 taken off at the end), 2 the max of C' - P2
+template <int R, int DPC, int I, int TRK>
 // A/B knobs of k_ocv_cost_fused, defaults as measured (profiles/r04_ocv_cost_ring_ab_v2.jsonl; cost stage,
 // 1080p block 5 / the shipped 2448x2048 D=480 block 21): the ring as bytes 0.234 -> 0.231 / 3.17 -> 3.01 ms,
 // plus <= 128 VGPRs asked for R > 9 (two blocks per CU at 36 B of spills) -> 2.86 ms; the box reads issued
@@ -721,7 +723,8 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             const int y = y0 + (v - 1) - 2 * SH2;
             const bool tail = last_band && y == fg_ncomp - 1;
             if constexpr (!kEarly) box_load(w);
-            u16x2_t sum = w[0];
+            // the window sum starts at P2, so the slid sum IS C' (mod 2^16, OpenCV's CostType wrap)
+            u16x2_t sum = w[0] + p2v;
 #pragma unroll
             for (int i = 1; i < R; i++) sum += w[i];
             // 32-bit element offsets off the uniform C' base (C' < 2^32 words: the launcher's
@@ -736,25 +739,27 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             for (int j = 0; j < L; j++) {
                 if (j > 0) sum += w[j + R - 1] - w[j - 1];
                 if (xa + j < xb) {
-                    if (!(col0 && xa + j == 0 && y > 0)) bmax = __builtin_elementwise_max(bmax, sum);
+                    if constexpr (TRK != 0)
+                        if (!(col0 && xa + j == 0 && y > 0))
+                            bmax = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
                     if constexpr (R <= SGM_FUSE_BUFST)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum + p2v), crow, (int)vb,
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), crow, (int)vb,
                                                               j * gD * 2, 0);
                     else
-                        C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum + p2v);
+                        C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum);
                 }
             }
             if (tail) {                                      // OpenCV's bottom rows: never recomputed
                 // (the row's values slid again from the registers: reading the stores back would
                 // put a vmcnt(0) wait into every row of the loop)
-                sum = w[0];
+                sum = w[0] + p2v;
 #pragma unroll
                 for (int i = 1; i < R; i++) sum += w[i];
                 uint32_t* o = C32 + ob;
 #pragma unroll
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
-                    const uint32_t c = fullDP ? gP2 * 0x10001u : __builtin_bit_cast(uint32_t, sum + p2v);
+                    const uint32_t c = fullDP ? gP2 * 0x10001u : __builtin_bit_cast(uint32_t, sum);
                     if (xa + j < xb)
                         for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
                     o += gD / 2;
@@ -767,8 +772,8 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
         }
         __syncthreads();
     }
-    if (gwide == 2 && govf && t < NB) {
-        const int m = max((int)bmax[0], (int)bmax[1]);
+    if (TRK != 0 && govf && t < NB) {
+        const int m = max((int)bmax[0], (int)bmax[1]) - (TRK == 1 ? gP2 : 0);
         const bool ovf = m > govf_thr - gP2;
         const uint64_t b = __ballot(ovf);
         if (b && (int)(threadIdx.x & 63) == __builtin_ctzll(b)) atomicOr(govf, 1);
@@ -1761,22 +1766,46 @@ static int fuse_dpc(const Geom& g)
     return dpc;
 }
 
-template <int R>
-static void launch_cost_fused_r(const uint32_t* bt, const Geom& g, int fullDP, const FuseGrid& fg, int16_t* C,
-                                hipStream_t st)
+// The overflow flag's tracking (k_ocv_cost_fused's TRK): none without the gate (Geom::wide != 2);
+// the max of C' when box + P2 stays below 2^16 for any pixels (a pixel cost is <= 2*ftzero + 63),
+// so the slid sum that starts at P2 is compared as it is stored; else the max of C' - P2
+static int ocv_fuse_track(const Geom& g)
+{
+    if (g.wide != 2) return 0;
+    const long long B = (long long)(2 * g.SW2 + 1) * (2 * g.SH2 + 1) * (2 * g.ftzero + 63);
+    return B + g.P2 <= 65535 ? 1 : 2;
+}
+
+template <int R, int TRK>
+static void launch_cost_fused_rt(const uint32_t* bt, const Geom& g, int fullDP, const FuseGrid& fg, int16_t* C,
+                                 hipStream_t st)
 {
     const dim3 grid(fg.per_xcd * 8), block(kFuseThreads);
     const int dpc = fuse_dpc(g);
     if constexpr (R <= 9) {
         if (dpc == 32) {
-            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8>), grid, block, FuseGeo(32).lds_bytes(32), st, bt, g, fullDP, fg, C);
+            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8, TRK>), grid, block, FuseGeo(32).lds_bytes(32), st, bt, g,
+                               fullDP, fg, C);
             return;
         }
     }
     if (dpc == 16)
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4>), grid, block, FuseGeo(16).lds_bytes(16), st, bt, g, fullDP, fg, C);
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4, TRK>), grid, block, FuseGeo(16).lds_bytes(16), st, bt, g, fullDP,
+                           fg, C);
     else
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2>), grid, block, FuseGeo(8).lds_bytes(8), st, bt, g, fullDP, fg, C);
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2, TRK>), grid, block, FuseGeo(8).lds_bytes(8), st, bt, g, fullDP,
+                           fg, C);
+}
+
+template <int R>
+static void launch_cost_fused_r(const uint32_t* bt, const Geom& g, int fullDP, const FuseGrid& fg, int16_t* C,
+                                hipStream_t st)
+{
+    switch (ocv_fuse_track(g)) {
+    case 0: launch_cost_fused_rt<R, 0>(bt, g, fullDP, fg, C, st); break;
+    case 1: launch_cost_fused_rt<R, 1>(bt, g, fullDP, fg, C, st); break;
+    default: launch_cost_fused_rt<R, 2>(bt, g, fullDP, fg, C, st); break;
+    }
 }
 
 static FuseGrid fuse_grid(const Geom& g)
