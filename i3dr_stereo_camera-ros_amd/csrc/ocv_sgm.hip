@@ -465,9 +465,19 @@ __global__ __launch_bounds__(256) void k_ocv_vsum_sat(const int16_t* __restrict_
 // in MODE_HH); COL0_LEGACY's column is written by k_ocv_col0_legacy afterwards.
 // Block ids are dealt XCD-aware: the DC-chunks of one tile (and then the next strip of the band)
 // run back to back on one XCD, so the partial lines of their C' rows merge in that L2.
-constexpr int kFuseThreads = 512;
-constexpr int kFuseNX = 128;              // staged columns per block: 4 threads per column
+#ifndef SGM_FUSE_NX
+#define SGM_FUSE_NX 128          // A/B: staged columns per block (256: 1024-thread blocks, one per CU)
+#endif
+constexpr int kFuseNX = SGM_FUSE_NX;      // staged columns per block: 4 threads per column
+constexpr int kFuseThreads = 4 * kFuseNX;
+constexpr int kFuseHalf = kFuseThreads / 2;   // waves 0 .. W/2 - 1: box (R > 9); the rest: staging
 __host__ __device__ inline int fuse_xb(const Geom& g) { return kFuseNX - 2 * g.SW2; }
+#ifndef SGM_FUSE_RB2
+#define SGM_FUSE_RB2 1           // A/B: two rows per barrier for boxes wider than 9 (0: one)
+#endif
+// rows per barrier: RB rows of pixel costs, boxes and staging between two barriers, the box RB
+// rows behind the pixel costs and the staging RB rows ahead, over 2 * RB LDS buffers each
+__host__ __device__ constexpr int fuse_rb(int R) { return (R > 9 && SGM_FUSE_RB2 != 0) ? 2 : 1; }
 struct FuseGeo {
     int DC, M, MH;
     __host__ __device__ FuseGeo(int dpc) {
@@ -480,8 +490,8 @@ struct FuseGeo {
         if (dpc == 32) MH += ((5 - MH % 8) + 8) % 8;
     }
     __host__ __device__ int stage_words() const { return 6 * kFuseNX + 14 * MH; }
-    __host__ __device__ size_t lds_bytes(int dpc) const {
-        return (size_t)4 * (2 * stage_words() + 2 * kFuseNX * dpc);
+    __host__ __device__ size_t lds_bytes(int dpc, int rb) const {
+        return (size_t)4 * 2 * rb * (stage_words() + kFuseNX * dpc);
     }
 };
 struct FuseGrid {
@@ -502,7 +512,7 @@ template <int R, int DPC, int I, int TRK>
 #define SGM_FUSE_BOX_EARLY 0     // the box reads issued before the pixel costs (else after the V store)
 #endif
 #ifndef SGM_FUSE_NB_WIDE
-#define SGM_FUSE_NB_WIDE 256     // A/B: box threads for R > 9 (512: every wave)
+#define SGM_FUSE_NB_WIDE kFuseHalf   // A/B: box threads for R > 9 (kFuseThreads: every wave)
 #endif
 #ifndef SGM_FUSE_RKOFF
 #define SGM_FUSE_RKOFF 1         // the right-entry LDS base kept opaque (read2 immediates, no add per read)
@@ -542,20 +552,23 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     const int y0 = band * fg_band_rows, y1 = min(fg_ncomp, y0 + fg_band_rows);
     const int nv = (y1 - y0) + 2 * SH2;                      // rows of P the band needs
     const int t = threadIdx.x;
-    uint32_t* S0 = lds_fuse;                                 // staging, two buffers
-    uint32_t* V0 = lds_fuse + 2 * fz.stage_words();          // V rows [NX][DPC], two buffers
+    constexpr int RB = fuse_rb(R), NBUF = 2 * RB;
+    uint32_t* S0 = lds_fuse;                                 // staging, NBUF buffers
+    uint32_t* V0 = lds_fuse + NBUF * fz.stage_words();       // V rows [NX][DPC], NBUF buffers
+    auto Sbuf = [&](int r) { return S0 + (r % NBUF) * fz.stage_words(); };
     const int xs = gminX1 + x0 - SW2;                       // staged column k <-> image x = xs + k
     const int xr0 = xs - gminD - (d0 + DC - 1);             // right entry r <-> xr0 + r
     const size_t plane = (size_t)gW * gH;
     // staging (waves 4-7, beside the box of waves 0-3): entry st of the 2 * NX left entries (one
-    // each) and entries st, st + 256 of the 2 * NRr right ones; the bt words of row v + 2 are
+    // each) and entries st, st + kFuseHalf of the 2 * NRr right ones; the bt words of row v + 2 are
     // loaded while row v + 1's are written to LDS, so a global load's latency spans a whole phase
-    const int st = t - 256;
+    const int st = t - kFuseHalf;
     const int NRr = NX + DC - 1;
     const int cl = st >= NX, kl = st - cl * NX;
     const int cr0 = st >= NRr, r0 = st - cr0 * NRr;
-    const bool has1 = st + 256 < 2 * NRr;
-    const int cr1 = st + 256 >= NRr, r1 = st + 256 - cr1 * NRr;
+    static_assert(2 * kFuseNX <= kFuseHalf, "one staging thread per left entry");
+    const bool has1 = st + kFuseHalf < 2 * NRr;
+    const int cr1 = st + kFuseHalf >= NRr, r1 = st + kFuseHalf - cr1 * NRr;
     // 32-bit element offsets off the uniform base (4 planes < 2^32 elements: the launcher's
     // condition), one register each instead of a 64-bit pointer
     const uint32_t oL = (uint32_t)(cl * plane) + (uint32_t)min(max(xs + kl, 0), gW - 1);
@@ -625,14 +638,16 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     const size_t rowC = (size_t)gw1 * gD / 2;         // u32 per C' row
     const bool last_band = y1 == fg_ncomp;
     int v_cur = 0;                                           // the row of the loop below
-    if (t >= 256) {
-        stage_load(0);
-        stage_store(S0);
-        if (1 < nv) stage_load(1);
+    if (t >= kFuseHalf) {
+        for (int r = 0; r < RB && r < nv; r++) {
+            stage_load(r);
+            stage_store(Sbuf(r));
+        }
+        if (RB < nv) stage_load(RB);
     }
     __syncthreads();
     auto box_load = [&](u16x2_t (&w)[NL]) __attribute__((always_inline)) {
-        const uint32_t* Vp = V0 + ((v_cur - 1) & 1) * NX * DPC + bp;
+        const uint32_t* Vp = V0 + ((v_cur - RB) % NBUF) * NX * DPC + bp;
         if (edge) {                                          // staged columns outside the frame: the edge column
 #pragma unroll
             for (int i = 0; i < NL; i++) w[i] = wd(Vp, min(max(xa + i, klo), khi) * DPC);
@@ -646,12 +661,11 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
         }
     };
     int slot = 0;
-    for (int v = 0; v <= nv; v++) {
+    for (int v = 0; v < nv + RB; v++) {
         v_cur = v;
-        uint32_t* S = S0 + (v & 1) * fz.stage_words();
-        // the box's window values of row v - 1 are read before the pixel costs of row v are
-        // computed (independent LDS buffers), so their latency hides behind that work
-        const bool dobox = t < NB && v >= 1 && v - 1 >= 2 * SH2 && xa < xb;
+        uint32_t* S = Sbuf(v);
+        // the box of row v - RB (its V written RB iterations ago, a barrier between)
+        const bool dobox = t < NB && v >= RB && v - RB >= 2 * SH2 && xa < xb;
         u16x2_t w[NL];
         if constexpr (kEarly)
             if (dobox) box_load(w);
@@ -707,7 +721,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             }
             slot = slot + 1 == R ? 0 : slot + 1;
             if (v >= 2 * SH2) {
-                uint32_t* Vout = V0 + (v & 1) * NX * DPC + kc * DPC + tq * I;
+                uint32_t* Vout = V0 + (v % NBUF) * NX * DPC + kc * DPC + tq * I;
                 // exactly the thread's I words (I = 2 at DPC = 8: one 8-byte store, 8-byte aligned)
                 if constexpr (I % 4 == 0) {
 #pragma unroll
@@ -719,8 +733,8 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 }
             }
         }
-        if (dobox) {                                         // the box of row v - 1
-            const int y = y0 + (v - 1) - 2 * SH2;
+        if (dobox) {                                         // the box of row v - RB
+            const int y = y0 + (v - RB) - 2 * SH2;
             const bool tail = last_band && y == fg_ncomp - 1;
             if constexpr (!kEarly) box_load(w);
             // the window sum starts at P2, so the slid sum IS C' (mod 2^16, OpenCV's CostType wrap)
@@ -766,11 +780,13 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 }
             }
         }
-        if (t >= 256 && v + 1 < nv) {
-            stage_store(S0 + ((v + 1) & 1) * fz.stage_words());
-            if (v + 2 < nv) stage_load(v + 2);
+        if (t >= kFuseHalf && v + RB < nv) {
+            stage_store(Sbuf(v + RB));
+            if (v + RB + 1 < nv) stage_load(v + RB + 1);
         }
-        __syncthreads();
+        // every write of iteration v is read RB iterations later and every buffer is rewritten
+        // 2 * RB iterations after its reads: one barrier per RB iterations orders both
+        if ((v + 1) % RB == 0) __syncthreads();
     }
     if (TRK != 0 && govf && t < NB) {
         const int m = max((int)bmax[0], (int)bmax[1]) - (TRK == 1 ? gP2 : 0);
@@ -1784,16 +1800,16 @@ static void launch_cost_fused_rt(const uint32_t* bt, const Geom& g, int fullDP, 
     const int dpc = fuse_dpc(g);
     if constexpr (R <= 9) {
         if (dpc == 32) {
-            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8, TRK>), grid, block, FuseGeo(32).lds_bytes(32), st, bt, g,
+            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8, TRK>), grid, block, FuseGeo(32).lds_bytes(32, fuse_rb(R)), st, bt, g,
                                fullDP, fg, C);
             return;
         }
     }
     if (dpc == 16)
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4, TRK>), grid, block, FuseGeo(16).lds_bytes(16), st, bt, g, fullDP,
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4, TRK>), grid, block, FuseGeo(16).lds_bytes(16, fuse_rb(R)), st, bt, g, fullDP,
                            fg, C);
     else
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2, TRK>), grid, block, FuseGeo(8).lds_bytes(8), st, bt, g, fullDP,
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2, TRK>), grid, block, FuseGeo(8).lds_bytes(8, fuse_rb(R)), st, bt, g, fullDP,
                            fg, C);
 }
 
@@ -1832,7 +1848,7 @@ static FuseGrid fuse_grid(const Geom& g)
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        slots = 2 * cus;
+        slots = (2 * 128 / kFuseNX) * cus;             // 512-thread blocks: two per CU
         if (dev < 64) slots_of[dev].store(slots, std::memory_order_relaxed);
     }
     const int min_rows = std::max(64, 8 * g.SH2);
