@@ -532,7 +532,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     // every Geom / FuseGrid field the kernel reads, as scalars: a by-value struct that any
     // lambda captures by reference is otherwise given an address (copied to scratch)
     const int gW = g.W, gH = g.H, gD = g.D, gP2 = g.P2, gw1 = g.width1, gminD = g.minD, gminX1 = g.minX1;
-    const int gSW2 = g.SW2, gSH2 = g.SH2, gcompat = g.compat, gwide = g.wide, govf_thr = g.ovf_thr;
+    const int gSW2 = g.SW2, gSH2 = g.SH2, gcompat = g.compat, govf_thr = g.ovf_thr;
     int* const govf = g.ovf;
     const int fg_strips = fg.strips, fg_chunks = fg.chunks, fg_band_rows = fg.band_rows, fg_ncomp = fg.ncomp;
     const int fg_total = fg.total, fg_per_xcd = fg.per_xcd;
@@ -1063,6 +1063,55 @@ __device__ __forceinline__ void load_vals(const VT* p, int (&v)[DPL])
     }
 }
 
+// Deficit planes (Geom::evol). In the plain int16 regime a path cost is L = C' - e with
+// e = (minLp + P2) - min(Lp(d), Lp(d -+ 1) + P1, minLp + P2) in [0, P2] (OpenCV's recurrence:
+// ocv_step_pk computes e on the way to L), so for P2 <= 511 a volume slot holds e in 9 bits
+// instead of L in 16: the D low bytes of a pixel and bit 8 of each as D/8 bytes (in each byte the
+// even d of a group of 8 at bits 0-3 and the odd ones at bits 4-7, the order the packed pairs
+// give), 9/8 B per cell instead of 2 written by the paths and read by the WTA; the readers load C'
+// beside them and rebuild L exactly. Two layouts (Geom::evol): 1 = one record per pixel
+// (9D/8 rounded up to 16 B: a path step writes one contiguous run), 2 = a byte plane then a bit
+// plane (D % 128 == 0: each pixel's low bytes are whole 128-B lines).
+struct EvLayout {
+    uint32_t ls, hs;        // bytes per pixel of the low bytes / of the bits
+    size_t hb;              // offset of pixel 0's bits in the slot
+};
+__host__ __device__ inline int evol_rs(int D) { return (9 * D / 8 + 15) & ~15; }
+__host__ __device__ inline EvLayout evol_layout(const Geom& g)
+{
+    if (g.evol == 2) return EvLayout{(uint32_t)g.D, (uint32_t)g.D / 8, (size_t)g.width1 * g.H * g.D};
+    const uint32_t rs = (uint32_t)evol_rs(g.D);
+    return EvLayout{rs, rs, (size_t)g.D};
+}
+__device__ __forceinline__ int evol_pos(int d) { return ((d & 1) << 2) | ((d & 7) >> 1); }
+// N consecutive e from d0 (a multiple of N): lo = the low byte of d0, hi = the bit byte holding
+// d0's bit
+template <int N>
+__device__ __forceinline__ void load_e(const uint8_t* lo, const uint8_t* hi, int d0, int (&e)[N])
+{
+    uint32_t w[(N + 3) / 4];
+    if constexpr (N == 1) w[0] = *lo;
+    else if constexpr (N == 2) w[0] = *(const uint16_t*)lo;
+    else if constexpr (N == 4) w[0] = *(const uint32_t*)lo;
+    else if constexpr (N == 8) { const uint2 t = *(const uint2*)lo; w[0] = t.x; w[1] = t.y; }
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 16; c++) {
+            const uint4 t = ((const uint4*)lo)[c];
+            w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
+        }
+    }
+    uint32_t h;                                          // bit planes are only 2-B aligned for N = 32
+    if constexpr (N <= 8) h = *hi;
+    else if constexpr (N == 16) h = *(const uint16_t*)hi;
+    else h = (uint32_t)((const uint16_t*)hi)[0] | ((uint32_t)((const uint16_t*)hi)[1] << 16);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int pos = N >= 8 ? evol_pos(k) + 8 * (k / 8) : evol_pos(d0 + k);
+        e[k] = (int)(((w[k / 4] >> (8 * (k % 4))) & 0xFFu) | (((h >> pos) & 1u) << 8));
+    }
+}
+
 // OpenCV recurrence of one cell with int16 storage semantics, for a path line held by LPL
 // lanes (16: one row of the wave; 32: two rows) — lane p: d = p*DPL .. p*DPL + DPL - 1.
 // Entries with d >= D hold kMaxCost (OpenCV's Lr[-1] / Lr[D] = MAX_COST padding).
@@ -1144,6 +1193,9 @@ constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 #ifndef SGM_OCV_VWTA_PK
 #define SGM_OCV_VWTA_PK 1  // k_ocv_vwta_pk for the plain int16 regime with uniqueness < 100
 #endif
+#ifndef SGM_OCV_VWTA_PK_EV5
+#define SGM_OCV_VWTA_PK_EV5 1  // k_ocv_vwta_pk also for MODE_SGBM when the volumes are deficit records
+#endif
 #ifndef SGM_OCV_VWTA_PK_PF
 #define SGM_OCV_VWTA_PK_PF 0  // k_ocv_vwta_pk steps in flight (0: by shape)
 #endif
@@ -1178,7 +1230,8 @@ __device__ __forceinline__ uint32_t line_shl1_u(uint32_t v, int p)      // lane 
 // its valid d (entries with d >= D are forced to kMaxCost = 32767 by imask, as OpenCV pads).
 template <int DPL, int LPL>
 __device__ __forceinline__ uint32_t ocv_step_pk(const uint32_t (&C2)[DPL / 2], uint32_t (&L2)[DPL / 2], uint32_t delta2,
-                                                uint32_t P1P1, const uint32_t (&imask)[DPL / 2], int p)
+                                                uint32_t P1P1, const uint32_t (&imask)[DPL / 2], int p,
+                                                uint32_t* E2 = nullptr)   // E2: the deficits e = C' - L
 {
     constexpr int M = DPL / 2;
     uint32_t q[M];
@@ -1191,7 +1244,9 @@ __device__ __forceinline__ uint32_t ocv_step_pk(const uint32_t (&C2)[DPL / 2], u
     for (int i = 0; i < M; i++) {
         const uint32_t On = (i + 1 < M) ? alignbit16(q[i + 1], q[i]) : alignbit16(Y, q[M - 1]);
         const uint32_t t = pk_min(pk_min(Op, On), pk_min(L2[i], delta2));
-        const uint32_t v = pk_sub(C2[i], pk_sub(delta2, t));
+        const uint32_t e = pk_sub(delta2, t);
+        if (E2) E2[i] = e;
+        const uint32_t v = pk_sub(C2[i], e);
         L2[i] = (v & ~imask[i]) | (0x7FFF7FFFu & imask[i]);
         mn = pk_min(mn, L2[i]);
         Op = On;
@@ -1209,6 +1264,36 @@ __device__ __forceinline__ void bload_dw(__amdgpu_buffer_rsrc_t rs, uint32_t off
             const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * c, 0, 0);
             w[4 * c] = t[0]; w[4 * c + 1] = t[1]; w[4 * c + 2] = t[2]; w[4 * c + 3] = t[3];
         }
+    }
+}
+
+// One step's deficits of a lane (DPL = 8 or 16 values, DPL / 2 packed pairs) into the deficit
+// planes: DPL low bytes at lo_off, DPL bits (evol_pos order) at hi_off; nontemporal, streamed once
+// into the WTA
+template <int DPL>
+__device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t lo_off, uint32_t hi_off,
+                                           const uint32_t (&E2)[DPL / 2])
+{
+    static_assert(DPL == 8 || DPL == 16, "one or two groups of 8 deficits per lane");
+    constexpr int NG = DPL / 8;
+    uint32_t lo[2 * NG], hb = 0;
+#pragma unroll
+    for (int c = 0; c < NG; c++) {
+        lo[2 * c] = __builtin_amdgcn_perm(E2[4 * c + 1], E2[4 * c], 0x06040200u);       // e(d0..d3) low bytes
+        lo[2 * c + 1] = __builtin_amdgcn_perm(E2[4 * c + 3], E2[4 * c + 2], 0x06040200u);
+        uint32_t t = 0;                                  // pair i: bit 8 of e(2i) -> bit i, of e(2i+1) -> 16 + i
+#pragma unroll
+        for (int i = 0; i < 4; i++) t |= as_u(as_v2(E2[4 * c + i]) >> (u16x2_t){8, 8}) << i;
+        hb |= ((t | (t >> 12)) & 0xFFu) << (8 * c);
+    }
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (NG == 1) {
+        __builtin_amdgcn_raw_buffer_store_b64((v2u){lo[0], lo[1]}, rs, lo_off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)hb, rs, hi_off, 0, 2);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){lo[0], lo[1], lo[2], lo[3]}, rs, lo_off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)hb, rs, hi_off, 0, 2);
     }
 }
 
@@ -1296,35 +1381,55 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             // 16 rows; the shipped D=480 config, M = 8: 6.20 ms unpacked and at 4 rows, 6.79 at 8;
             // profiles/r05_ocv_pk_ab.jsonl)
             constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? 4 : 2;
-            uint32_t C2[PF][M], L2[M];
+            // deficits (Geom::evol, 8 or 16 values per lane): the low bytes and the bits of d
+            const EvLayout el = evol_layout(g);
+            const long long pix0 = (long long)ybase * g.width1 + x0, pstep = (long long)ry * g.width1 + rx;
+            uint32_t ev_lo = (uint32_t)(pix0 * el.ls + dl), ev_hi = (uint32_t)(el.hb + pix0 * el.hs + dl / 8);
+            const uint32_t ev_step = (uint32_t)(pstep * el.ls), ev_hstep = (uint32_t)(pstep * el.hs);
+            auto run = [&](auto evc) {
+                constexpr bool EV = decltype(evc)::value;
+                uint32_t C2[PF][M], L2[M];
 #pragma unroll
-            for (int i = 0; i < M; i++) L2[i] = 0;
-            uint32_t delta2 = P2 * 0x10001u;             // the path's first pixel: L = C - P2
+                for (int i = 0; i < M; i++) L2[i] = 0;
+                uint32_t delta2 = P2 * 0x10001u;         // the path's first pixel: L = C - P2
 #pragma unroll
-            for (int q = 0; q < PF; q++) { bload_dw<M>(rsC, ld_b, C2[q]); ld_b += bstep; }
-            auto steps = [&](int i0) {
+                for (int q = 0; q < PF; q++) { bload_dw<M>(rsC, ld_b, C2[q]); ld_b += bstep; }
+                auto steps = [&](int i0) {
 #pragma unroll
-                for (int q = 0; q < PF; q++) {
-                    const int i = i0 + q;
-                    const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2[q], L2, delta2, P1P1, imask, p);
-                    const bool ok = lane_act && i < n;
-                    if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
-                        bstore_dw<8>(rsV, ok ? st_b : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
-                        bstore_dw<8>(rsV, ok && !straddle ? st_b + 32u : kBufDrop,
-                                     *reinterpret_cast<const uint32_t(*)[8]>(&L2[8]));
-                    } else {
-                        bstore_dw<M>(rsV, ok ? st_b : kBufDrop, L2);
+                    for (int q = 0; q < PF; q++) {
+                        const int i = i0 + q;
+                        uint32_t E2[M];
+                        const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2[q], L2, delta2, P1P1, imask, p, EV ? E2 : nullptr);
+                        const bool ok = lane_act && i < n;
+                        if constexpr (EV) {
+                            evol_store<DPL>(rsV, ok ? ev_lo : kBufDrop, ok ? ev_hi : kBufDrop, E2);
+                            ev_lo += ev_step;
+                            ev_hi += ev_hstep;
+                        } else if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
+                            bstore_dw<8>(rsV, ok ? st_b : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
+                            bstore_dw<8>(rsV, ok && !straddle ? st_b + 32u : kBufDrop,
+                                         *reinterpret_cast<const uint32_t(*)[8]>(&L2[8]));
+                        } else {
+                            bstore_dw<M>(rsV, ok ? st_b : kBufDrop, L2);
+                        }
+                        delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
+                        bload_dw<M>(rsC, ld_b, C2[q]);
+                        st_b += bstep;
+                        ld_b += bstep;
                     }
-                    delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
-                    bload_dw<M>(rsC, ld_b, C2[q]);
-                    st_b += bstep;
-                    ld_b += bstep;
+                };
+                for (int i0 = 0; i0 < nmax; i0 += PF) {
+                    if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+                    steps(i0);
                 }
             };
-            for (int i0 = 0; i0 < nmax; i0 += PF) {
-                if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
-                steps(i0);
+            if constexpr (DPL == 8 || DPL == 16) {
+                if (g.evol) {
+                    run(std::true_type{});
+                    return;
+                }
             }
+            run(std::false_type{});
             return;
         }
     }
@@ -1454,9 +1559,10 @@ __device__ __forceinline__ int wta_untie(int t, bool lane, int bits)
 // (SURVEY Appendix A.6): S = the saturating sums in OpenCV's pass order; best = first minimal d through
 // one 16-lane min over (S + 32768) * 512 + d; uniqueness per element (S may be any int16
 // here); S[best +- 1] through a per-row LDS slice; then the shared disp2 / LR epilogue.
-template <int DPL, int NDIR, typename VT, bool SAT>
+template <int DPL, int NDIR, typename VT, bool SAT, bool EV>
 __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, size_t vol_elems, Geom g,
-                                                   int16_t* __restrict__ out, size_t out_stride)
+                                                   int16_t* __restrict__ out, size_t out_stride,
+                                                   const int16_t* __restrict__ Cv)   // C' (EV: deficit planes)
 {
     if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
     const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
@@ -1475,9 +1581,25 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, 
     // pixel 4q + r; the last group reads up to 3 pixels past the row (the next row or the
     // volume slack), results never stored
     auto load = [&](int q, int (&v)[NDIR][DPL]) {
-        const VT* base = vols + row0 + (size_t)(4 * q + r) * g.D + dl;
+        const size_t cell = row0 + (size_t)(4 * q + r) * g.D + dl;
+        if constexpr (EV) {                              // L = C' - e
+            int16_t c[DPL];
+            load_i16<DPL>(Cv + cell, c);
+            const EvLayout el = evol_layout(g);
+            const size_t px = (size_t)y * g.width1 + 4 * q + r;
 #pragma unroll
-        for (int k = 0; k < NDIR; k++) load_vals<VT, DPL>(base + (size_t)k * vol_elems, v[k]);
+            for (int k = 0; k < NDIR; k++) {
+                const uint8_t* vb = (const uint8_t*)(vols + (size_t)k * vol_elems);
+                int e[DPL];
+                load_e<DPL>(vb + px * el.ls + dl, vb + el.hb + px * el.hs + dl / 8, dl, e);
+#pragma unroll
+                for (int j = 0; j < DPL; j++) v[k][j] = c[j] - e[j];
+            }
+        } else {
+            const VT* base = vols + cell;
+#pragma unroll
+            for (int k = 0; k < NDIR; k++) load_vals<VT, DPL>(base + (size_t)k * vol_elems, v[k]);
+        }
     };
     int nxt[NDIR][DPL];
     load(min(w, nq - 1), nxt);
@@ -1598,7 +1720,7 @@ __global__ __launch_bounds__(256) void k_ocv_wta64(const VT* __restrict__ vols, 
 // best = -1) go to res; k_census_rowfin finishes the rows (disp2 + LR, the shared row_finish).
 // A column is a sequential chain of H steps and there are only width1 of them, so this pays
 // on tall frames with many columns (the shipped 2448x2048 config), not on small ones.
-template <int DPL, int NDIR, typename VT, bool SAT>
+template <int DPL, int NDIR, typename VT, bool SAT, bool EV>
 __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, const VT* __restrict__ vols,
                                                  size_t vol_elems, Geom g, uint64_t* __restrict__ res, int use_pk)
 {
@@ -1619,12 +1741,25 @@ __global__ __launch_bounds__(64) void k_ocv_vwta(const int16_t* __restrict__ C, 
     };
     auto load = [&](int i, int (&c)[DPL], int (&v)[NDIR][DPL]) {
         int16_t t[DPL];
-        load_i16<DPL>(C + cell(i), t);
+        const size_t ci = cell(i);
+        const EvLayout el = evol_layout(g);
+        const size_t px = (size_t)(F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0)) * g.width1 + x1;
+        load_i16<DPL>(C + ci, t);
 #pragma unroll
         for (int k = 0; k < DPL; k++) c[k] = t[k];
 #pragma unroll
-        for (int s = 0; s < NDIR; s++)
-            if (s != F) load_vals<VT, DPL>(vols + (size_t)s * vol_elems + cell(i), v[s]);
+        for (int s = 0; s < NDIR; s++) {
+            if (s == F) continue;
+            if constexpr (EV) {                          // L = C' - e (deficit planes)
+                const uint8_t* vb = (const uint8_t*)(vols + (size_t)s * vol_elems);
+                int e[DPL];
+                load_e<DPL>(vb + px * el.ls + dl, vb + el.hb + px * el.hs + dl / 8, dl, e);
+#pragma unroll
+                for (int k = 0; k < DPL; k++) v[s][k] = c[k] - e[k];
+            } else {
+                load_vals<VT, DPL>(vols + (size_t)s * vol_elems + ci, v[s]);
+            }
+        }
     };
     int Lp[DPL], mLp = 0, Cq[PF][DPL], Vq[PF][NDIR][DPL];
 #pragma unroll
@@ -2021,6 +2156,39 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
     return waves < kOcvWideLineWaves ? 32 : 16;
 }
 
+// the values per lane launch_ocv_paths picks for the frame
+static int ocv_paths_dpl(const Geom& g, int dirmask)
+{
+    const int D = g.D, lpl = ocv_lanes_per_line(g, dirmask);
+    if (lpl == 64) return D <= 512 ? 8 : D <= 1024 ? 16 : 32;
+    if (lpl == 32) return D <= 64 ? 2 : D <= 128 ? 4 : D <= 256 ? 8 : 16;
+    return dpl_for(D);
+}
+
+// Deficits (Geom::evol, load_e) for the plain kernels of a frame: P2 <= 511 (e in 9 bits), the
+// packed paths step (P1 <= 32768) with buffer offsets, 8 or 16 values per path lane (whole groups
+// of 8 per lane), D <= 512 (the row WTA k_ocv_wta16 or the fused vertical WTA read them). Returns
+// the layout (1 records, 2 planes for D % 128 == 0) or 0; SGM_OCV_EVOL=0 (environment or build
+// macro) keeps int16 L volumes, =1 / =2 forces a layout.
+#ifndef SGM_OCV_EVOL
+#define SGM_OCV_EVOL 1
+#endif
+int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
+{
+    if (SGM_OCV_EVOL == 0 || SGM_OCV_PK == 0) return 0;
+    const char* e = std::getenv("SGM_OCV_EVOL");       // 0 off, 1 / 2 force a layout
+    if (e && std::atoi(e) == 0) return 0;
+    if (g.wide == 1 || g.P2 > 511 || g.P1 > 32768 || g.D > 512 || g.width1 <= 0) return 0;
+    if ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF")) return 0;
+    const int dpl = ocv_paths_dpl(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
+    if (dpl != 8 && dpl != 16) return 0;
+    // the fused vertical WTA reads them from 8 values per lane (D > 256): with 2 or 4 the byte and
+    // bit loads per direction cost more than they save (1080p D=128 MODE_HH 2.48 -> 2.95 ms)
+    if (skipdir >= 0 && g.D <= 256) return 0;
+    if (e && (std::atoi(e) == 1 || std::atoi(e) == 2)) return std::atoi(e);
+    return g.D % 128 == 0 ? 2 : 1;
+}
+
 hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
                             int dirmask, hipStream_t st, int skipdir)
 {
@@ -2047,21 +2215,35 @@ hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, s
     return hipGetLastError();
 }
 
-template <int DPL, typename VT, bool SAT>
-static void launch_ocv_wta_dpl(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
-                               size_t out_stride, hipStream_t st)
+template <int DPL, typename VT, bool SAT, bool EV>
+static void launch_ocv_wta_e(const int16_t* C, const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
+                             size_t out_stride, hipStream_t st)
 {
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
     const VT* v = (const VT*)vols;
     if (ndir == 8)
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT, SAT, EV>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out,
+                           out_stride, C);
     else
-        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
+        hipLaunchKernelGGL((k_ocv_wta16<DPL, 5, VT, SAT, EV>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out,
+                           out_stride, C);
+}
+template <int DPL, typename VT, bool SAT>
+static void launch_ocv_wta_dpl(const int16_t* C, const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
+                               size_t out_stride, hipStream_t st)
+{
+    if constexpr (!SAT && sizeof(VT) == 2) {
+        if (g.evol) {
+            launch_ocv_wta_e<DPL, VT, SAT, true>(C, vols, cells, ndir, g, out, out_stride, st);
+            return;
+        }
+    }
+    launch_ocv_wta_e<DPL, VT, SAT, false>(C, vols, cells, ndir, g, out, out_stride, st);
 }
 
 template <typename VT, bool SAT>
-static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
+static void launch_ocv_wta_t(const int16_t* C, const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                              size_t out_stride, hipStream_t st)
 {
     const int D = g.D;
@@ -2075,23 +2257,25 @@ static void launch_ocv_wta_t(const void* vols, size_t cells, int ndir, const Geo
             hipLaunchKernelGGL((k_ocv_wta64<5, VT, SAT>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out, out_stride);
         return;
     }
-    if (D <= 32) launch_ocv_wta_dpl<2, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 64) launch_ocv_wta_dpl<4, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 128) launch_ocv_wta_dpl<8, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
-    else if (D <= 256) launch_ocv_wta_dpl<16, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_dpl<32, VT, SAT>(vols, cells, ndir, g, out, out_stride, st);
+    if (D <= 32) launch_ocv_wta_dpl<2, VT, SAT>(C, vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 64) launch_ocv_wta_dpl<4, VT, SAT>(C, vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 128) launch_ocv_wta_dpl<8, VT, SAT>(C, vols, cells, ndir, g, out, out_stride, st);
+    else if (D <= 256) launch_ocv_wta_dpl<16, VT, SAT>(C, vols, cells, ndir, g, out, out_stride, st);
+    else launch_ocv_wta_dpl<32, VT, SAT>(C, vols, cells, ndir, g, out, out_stride, st);
 }
 
 // vols: int16 volumes (wide 0), the flagged kind (wide 1: int32, or saturating int16 under
 // SIMD_SAT), or a region sized for the larger, read as the one the cost kernel's overflow
 // flag selects (wide 2); cells = width1 * H * D per volume
-hipError_t launch_ocv_wta(const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
+hipError_t launch_ocv_wta(const int16_t* C, const void* vols, size_t cells, int ndir, const Geom& g, int16_t* out,
                           size_t out_stride, hipStream_t st)
 {
-    if (g.wide != 1) launch_ocv_wta_t<int16_t, false>(vols, cells, ndir, g, out, out_stride, st);
+    if (g.wide != 1) launch_ocv_wta_t<int16_t, false>(C, vols, cells, ndir, g, out, out_stride, st);
     if (g.wide == 0) return hipGetLastError();
-    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_wta_t<int16_t, true>(vols, cells, ndir, g, out, out_stride, st);
-    else launch_ocv_wta_t<int32_t, false>(vols, cells, ndir, g, out, out_stride, st);
+    Geom gf = g;
+    gf.evol = 0;                                         // the flagged kernels keep full volumes
+    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_wta_t<int16_t, true>(C, vols, cells, ndir, gf, out, out_stride, st);
+    else launch_ocv_wta_t<int32_t, false>(C, vols, cells, ndir, gf, out, out_stride, st);
     return hipGetLastError();
 }
 
@@ -2135,7 +2319,24 @@ __device__ __forceinline__ void load_dw(const int16_t* p, uint32_t (&w)[N])
         }
     }
 }
-template <int DPL, int NDIR>
+// The packed pairs of the lane's deficits (Geom::evol) from its raw loads: w[0 .. M/2) the byte
+// plane's dwords, w[M/2] the bit-plane bytes (DPL = 8 or 16)
+template <int M>
+__device__ __forceinline__ void evol_pairs(const uint32_t (&w)[M], uint32_t (&e2)[M])
+{
+#pragma unroll
+    for (int c = 0; c < M / 4; c++) {
+        // evens of the group at bits 0-3, odds at bits 16-19
+        const uint32_t hb = (w[M / 2] >> (8 * c)) & 0xFFu;
+        const uint32_t h2 = (hb * 0x1001u) & 0x000F000Fu;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t lo2 = __builtin_amdgcn_perm(0u, w[2 * c + i / 2], (i & 1) ? 0x0C030C02u : 0x0C010C00u);
+            e2[4 * c + i] = ((h2 << (8 - i)) & 0x01000100u) | lo2;
+        }
+    }
+}
+template <int DPL, int NDIR, bool EV>
 __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ C, const int16_t* __restrict__ vols,
                                                     size_t vol_elems, Geom g, uint64_t* __restrict__ res)
 {
@@ -2154,12 +2355,32 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
         const int y = F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0);
         return ((size_t)y * g.width1 + x1) * g.D + dl;
     };
+    static_assert(!EV || DPL == 8 || DPL == 16, "deficit planes: 8 or 16 values per lane");
     auto load = [&](int i, uint32_t (&c)[M], uint32_t (&v)[NDIR][M]) {
         const size_t o = cell(i);
         load_dw<M>(C + o, c);
+        const EvLayout el = evol_layout(g);
+        const size_t px = (size_t)(F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0)) * g.width1 + x1;
 #pragma unroll
-        for (int s = 0; s < NDIR; s++)
-            if (s != F) load_dw<M>(vols + (size_t)s * vol_elems + o, v[s]);
+        for (int s = 0; s < NDIR; s++) {
+            if (s == F) continue;
+            if constexpr (EV) {                          // raw: byte-plane dwords, then the bit-plane bytes
+                const uint8_t* vb = (const uint8_t*)(vols + (size_t)s * vol_elems);
+                const uint8_t* lo = vb + px * el.ls + dl;
+                const uint8_t* hi = vb + el.hb + px * el.hs + dl / 8;
+                if constexpr (DPL == 8) {
+                    const uint2 t = *(const uint2*)lo;
+                    v[s][0] = t.x; v[s][1] = t.y;
+                    v[s][2] = *hi;
+                } else {
+                    const uint4 t = *(const uint4*)lo;
+                    v[s][0] = t.x; v[s][1] = t.y; v[s][2] = t.z; v[s][3] = t.w;
+                    v[s][4] = *(const uint16_t*)hi;
+                }
+            } else {
+                load_dw<M>(vols + (size_t)s * vol_elems + o, v[s]);
+            }
+        }
     };
     uint32_t imask[M], tie[M][2];
 #pragma unroll
@@ -2181,14 +2402,27 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
     auto step = [&](int i, const uint32_t (&Cc)[M], const uint32_t (&V)[NDIR][M]) {
         const uint32_t lmin = ocv_step_pk<DPL, LPL>(Cc, L2, delta2, P1P1, imask, p);
         delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
-        uint32_t S2[M];
+        uint32_t S2[M], Lv[NDIR][M];                    // the other directions' L of the cell
+#pragma unroll
+        for (int s = 0; s < NDIR; s++) {
+            if (s == F) continue;
+            if constexpr (EV) {
+                uint32_t e2[M];
+                evol_pairs<M>(V[s], e2);
+#pragma unroll
+                for (int j = 0; j < M; j++) Lv[s][j] = pk_sub(Cc[j], e2[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < M; j++) Lv[s][j] = V[s][j];
+            }
+        }
         int km = 0x7FFFFFFF;
 #pragma unroll
         for (int j = 0; j < M; j++) {
             s16x2_t a = __builtin_bit_cast(s16x2_t, L2[j]);
 #pragma unroll
             for (int s = 0; s < NDIR; s++)
-                if (s != F) a = __builtin_elementwise_add_sat(a, __builtin_bit_cast(s16x2_t, V[s][j]));
+                if (s != F) a = __builtin_elementwise_add_sat(a, __builtin_bit_cast(s16x2_t, Lv[s][j]));
             S2[j] = __builtin_bit_cast(uint32_t, a) | imask[j];
             const int klo = (int)(((S2[j] & 0xFFFFu) << 11) | tie[j][0]);
             const int khi = (int)(((S2[j] >> 16) << 11) | tie[j][1]);
@@ -2260,15 +2494,29 @@ static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, 
     // and 1080p MODE_HH (0.87 vs 0.90-0.94) keep k_ocv_vwta (profiles/r05_ocv_vwta_pk_ab.jsonl):
     // the kernel streams its volumes near the read peak, and fewer instructions help only where
     // the operands of more steps fit in flight
-    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 8 && NDIR == 8) {
-        if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0) {
-            hipLaunchKernelGGL((k_ocv_vwta_pk<DPL, NDIR>), dim3(g.width1), dim3(64), 0, st, C, (const int16_t*)vols,
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 8) {
+        if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0 && (NDIR == 8 || (g.evol && SGM_OCV_VWTA_PK_EV5))) {
+            if constexpr (DPL <= 16) {
+                if (g.evol) {
+                    hipLaunchKernelGGL((k_ocv_vwta_pk<DPL, NDIR, true>), dim3(g.width1), dim3(64), 0, st, C,
+                                       (const int16_t*)vols, vol_elems, g, res);
+                    return;
+                }
+            }
+            hipLaunchKernelGGL((k_ocv_vwta_pk<DPL, NDIR, false>), dim3(g.width1), dim3(64), 0, st, C, (const int16_t*)vols,
                                vol_elems, g, res);
             return;
         }
     }
-    hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols, vol_elems,
-                       g, res, use_pk);
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL <= 16) {
+        if (g.evol) {
+            hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT, true>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols,
+                               vol_elems, g, res, use_pk);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_ocv_vwta<DPL, NDIR, VT, SAT, false>), dim3(g.width1), dim3(64), 0, st, C, (const VT*)vols,
+                       vol_elems, g, res, use_pk);
 }
 template <int DPL, int NDIR>
 static void launch_ocv_vwta_v(const int16_t* C, const int16_t* Csat, const void* vols, size_t cells, const Geom& g,

@@ -56,7 +56,8 @@ hipError_t launch_ocv_paths(const int16_t*, const int16_t*, void*, size_t, const
                             int skipdir = -1);
 hipError_t launch_ocv_vwta(const int16_t*, const int16_t*, const void*, size_t, int, const Geom&, uint64_t*, hipStream_t);
 int ocv_vwta_dir(int ndir);
-hipError_t launch_ocv_wta(const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
+hipError_t launch_ocv_wta(const int16_t*, const void*, size_t, int, const Geom&, int16_t*, size_t, hipStream_t);
+int ocv_evol_mode(const Geom&, int, int);
 }  // namespace sgm
 
 using sgm::Geom;
@@ -558,9 +559,13 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
             HIP_TRY(hipMemsetAsync(gg.ovf, 0, sizeof(int), st), "hipMemsetAsync");
         }
         const double es = g.wide == 1 && !(g.compat & SGM_OCV_SIMD_SAT) ? 4 : 2;   // gated: the int16 case
+        const bool vwta = ocv_vwta_on(g, fullDP);
+        // the plain kernels' volumes as deficit planes where they fit (the stage byte bases below stay
+        // those of int16 volumes)
+        gg.evol = sgm::ocv_evol_mode(gg, mask, vwta ? sgm::ocv_vwta_dir(ndir) : -1);
         rec.begin("ocv_cost", 2 * WH + 2 * cells);
         HIP_TRY(sgm::launch_ocv_cost(dL, dR, stride, gg, fullDP, (uint8_t*)(ws + l.planes), A, B, st), "ocv_cost");
-        if (ocv_vwta_on(g, fullDP)) {
+        if (vwta) {
             // the vertical direction of the last group fused with the WTA (k_ocv_vwta), then
             // disp2 + LR of each row from the per-pixel results (the census rowfin)
             const int fd = sgm::ocv_vwta_dir(ndir);
@@ -578,7 +583,7 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
             rec.begin("ocv_paths", 2 * cells + es * cells * ndir);
             HIP_TRY(sgm::launch_ocv_paths(A, A, V, ncells, gg, mask, st), "ocv_paths");
             rec.begin("ocv_wta_lr", es * cells * ndir + 2 * WH);
-            HIP_TRY(sgm::launch_ocv_wta(V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
+            HIP_TRY(sgm::launch_ocv_wta(A, V, ncells, ndir, gg, dst, dst_stride, st), "ocv_wta");
         }
     }
     int rc = run_post(h, l, g, dOut, out_stride, rec);

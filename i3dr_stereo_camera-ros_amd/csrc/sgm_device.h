@@ -49,6 +49,8 @@ struct Geom {
     int compat;             // OCV: SGM_OCV_* bits (sgm_params.ocv_compat); census: 0
     int ovf_thr;            // OCV: largest C' the plain kernels reproduce exactly (32767, or
                             // 32767 - P2 under SIMD_SAT: (short)(minLr + P2) must not wrap)
+    int evol;               // OCV: the plain kernels' path volumes hold deficit planes (C' - L in
+                            // 9 bits: ocv_evol_ok) instead of int16 L
 };
 
 // OCV workspace: the four u8 prefilter planes, then (256-B aligned) the four u32 planes of
