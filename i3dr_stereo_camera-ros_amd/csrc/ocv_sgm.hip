@@ -1193,6 +1193,9 @@ constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 #ifndef SGM_OCV_VWTA_PK
 #define SGM_OCV_VWTA_PK 1  // k_ocv_vwta_pk for the plain int16 regime with uniqueness < 100
 #endif
+#ifndef SGM_OCV_ILV
+#define SGM_OCV_ILV 1  // k_ocv_paths: the directions' blocks dealt round-robin for 64-lane lines (env SGM_OCV_ILV overrides)
+#endif
 #ifndef SGM_OCV_VWTA_PK_EV5
 #define SGM_OCV_VWTA_PK_EV5 1  // k_ocv_vwta_pk also for MODE_SGBM when the volumes are deficit records
 #endif
@@ -1306,17 +1309,33 @@ __device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t l
 template <int DPL, int LPL, typename VT, bool SAT>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, VT* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
-                                                  int4 nblk1, int use_buf, int use_pk)
+                                                  int4 nblk1, int use_buf, int use_pk, int ilv)
 {
     if (ocv_gate_skip<SAT || sizeof(VT) == 4>(g)) return;
     const int nb[8] = {nblk0.x, nblk0.y, nblk0.z, nblk0.w, nblk1.x, nblk1.y, nblk1.z, nblk1.w};
-    // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask
+    // block -> (direction, group of 4 lines); volume slot = rank of the direction in dirmask.
+    // ilv: the directions' blocks dealt round-robin (block b: the (b mod n)-th direction with
+    // blocks, its group b / n; groups past a direction's count exit), so the lines of every
+    // direction that start together run together
     int b = blockIdx.x, dir = 0, slot = 0;
-    for (int i = 0; i < 8; i++) {
-        if (!((dirmask >> i) & 1)) continue;
-        if (b < nb[i]) { dir = i; break; }
-        b -= nb[i];
-        slot++;
+    if (ilv) {
+        int nact = 0;
+        for (int i = 0; i < 8; i++) nact += nb[i] > 0;
+        const int k = b % nact;
+        b /= nact;
+        for (int i = 0, c = 0; i < 8; i++) {
+            if (!((dirmask >> i) & 1)) continue;
+            if (nb[i] > 0 && c++ == k) { dir = i; break; }
+            slot++;
+        }
+        if (b >= nb[dir]) return;
+    } else {
+        for (int i = 0; i < 8; i++) {
+            if (!((dirmask >> i) & 1)) continue;
+            if (b < nb[i]) { dir = i; break; }
+            b -= nb[i];
+            slot++;
+        }
     }
     VT* V = vols + (size_t)slot * vol_elems;
     constexpr int NLW = 64 / LPL;                      // lines per wave
@@ -2097,14 +2116,24 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
     int ndir = 0;
     for (int i = 0; i < 8; i++) ndir += (dirmask >> i) & 1;
     const size_t trash_off = (size_t)ndir * vol_elems;
-    int nb[8], total = 0;
+    int nb[8], total = 0, nact = 0, nbmax = 0;
     for (int i = 0; i < 8; i++) {
         nb[i] = 0;
         if (!((dirmask >> i) & 1)) continue;
         const int lines = dir_ry(i) == 0 ? g.H : g.width1 + (dir_rx(i) != 0 ? g.H - 1 : 0);
         nb[i] = i == skipdir ? 0 : (lines + 64 / LPL - 1) / (64 / LPL);
         total += nb[i];
+        nact += nb[i] > 0;
+        nbmax = std::max(nbmax, nb[i]);
     }
+    // directions dealt round-robin for 64-lane lines (one line per wave, D > 256): the diagonal
+    // lines that start on the top row together read each C' row at about the same time, the
+    // second read served by the caches (the shipped 2448x2048 D=480 MODE_SGBM paths 5.30 -> 4.16 ms,
+    // MODE_HH 9.78 -> 9.57; 1080p D=128, 16-lane lines: 0.81 -> 0.83 and 1.16 -> 1.22, so not there;
+    // profiles/r05_ocv_ilv_ab.jsonl). SGM_OCV_ILV=0 / 1 forces it.
+    const char* ie = getenv("SGM_OCV_ILV");
+    const int ilv = (ie ? atoi(ie) != 0 : SGM_OCV_ILV != 0 && LPL == 64) && nact > 1;
+    if (ilv) total = nact * nbmax;
     const int4 a = make_int4(nb[0], nb[1], nb[2], nb[3]), b = make_int4(nb[4], nb[5], nb[6], nb[7]);
     // 32-bit buffer offsets when a volume ends below kBufDrop (the shipped 2448x2048 D=480
     // config's int16 volumes are 3.6 GB; SGM_OCV_NO_BUF=1 forces the 64-bit path)
@@ -2113,7 +2142,7 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
     const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
     if (total > 0)
         hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
-                       dirmask, a, b, use_buf, use_pk);
+                       dirmask, a, b, use_buf, use_pk, ilv);
 }
 
 // the plain kernels (wide != 1) and the flagged ones (wide != 0): int32 volumes for the scalar
