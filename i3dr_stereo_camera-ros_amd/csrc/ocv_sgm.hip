@@ -1666,6 +1666,229 @@ __global__ __launch_bounds__(256) void k_ocv_wta16(const VT* __restrict__ vols, 
     row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
 }
 
+// N dwords (2N int16) from p
+template <int N>
+__device__ __forceinline__ void load_dw(const int16_t* p, uint32_t (&w)[N])
+{
+    if constexpr (N == 1) w[0] = *(const uint32_t*)p;
+    else if constexpr (N == 2) { const uint2 t = *(const uint2*)p; w[0] = t.x; w[1] = t.y; }
+    else {
+#pragma unroll
+        for (int c = 0; c < N / 4; c++) {
+            const uint4 t = ((const uint4*)p)[c];
+            w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
+        }
+    }
+}
+
+// k_ocv_wta16 in packed u16 pairs for the plain int16 regime (no flagged frame, uniqueness
+// ratio < 100), the same rows, lanes and decisions. Every path cost there lies in [0, 32767], so
+// OpenCV's S = sat16(sat16(s1) + s2) is min(sum, 32767) in any order: saturating packed i16 adds
+// of the loaded dwords. With deficit volumes (EV: L = C' - e, e <= P2 <= 511 <= C') the sum is
+// S = min(NDIR * C' - E, 32767) with E = the sum of the NDIR deficits (<= 4088, exact in u16),
+// and with C' clamped first to Cc = ceil((32767 + NDIR * P2) / NDIR) (NDIR * Cc <= 36856 in u16)
+// the clamp gives the same S: the deficits are summed as raw bytes and bits before any unpacking,
+// in an even / odd split of each group of 8 (dword h of a group: (d 4h, d 4h + 2) for the evens,
+// (d 4h + 1, d 4h + 3) for the odds), and C' is permuted into that order instead. Entries with
+// d >= D are forced to 0xFFFF, above every real S. best and minS from one 16-lane min over
+// S << 9 | tie(d); uniqueness as a count (k_ocv_vwta_pk): the number of d with S < T =
+// ceil(minS * 100 / (100 - u)) against the count inside {best - 1, best, best + 1}.
+#ifndef SGM_OCV_WTA_PK
+#define SGM_OCV_WTA_PK 1   // the packed row WTA for the plain int16 regime (0: k_ocv_wta16 everywhere)
+#endif
+template <int DPL, bool EV>
+__device__ __forceinline__ int wta_pk_d(int k, int h)   // d - dl of half h of dword k of a lane
+{
+    if constexpr (EV) {
+        const int gi = k / 4, kk = k % 4;
+        return 8 * gi + ((kk & 2) ? 1 : 0) + 4 * (kk & 1) + 2 * h;
+    } else {
+        return 2 * k + h;
+    }
+}
+template <int DPL, int NDIR, bool EV>
+__global__ __launch_bounds__(256) void k_ocv_wta16_pk(const int16_t* __restrict__ vols, size_t vol_elems, Geom g,
+                                                      int16_t* __restrict__ out, size_t out_stride,
+                                                      const int16_t* __restrict__ Cv)   // C' (EV: deficit planes)
+{
+    if (ocv_gate_skip<false>(g)) return;
+    constexpr int M = DPL / 2;
+    static_assert(!EV || DPL == 8 || DPL == 16, "deficit planes: 8 or 16 values per lane");
+    constexpr int NG = DPL / 8;                          // EV: groups of 8 per lane
+    // raw words per direction: plain M dwords; EV the low-byte dwords, then the bit bytes
+    constexpr int NW = EV ? DPL / 4 + 1 : M;
+    const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
+    extern __shared__ uint32_t lds_ocv[];
+    uint32_t* sl = lds_ocv;                              // 16 lane rows x 16 lanes x M dwords of S
+    RowLds R((char*)lds_ocv + (size_t)16 * 16 * DPL * 2, g.W);
+    const int tid = threadIdx.x, lane = tid & 63, y = blockIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane >> 4, p = lane & 15;
+    R.init(g, tid, 256);
+    const bool lane_act = p * DPL < g.D;
+    const int dl = lane_act ? p * DPL : 0;
+    uint32_t* srow = sl + (w * 4 + r) * 16 * M;
+    const int n = g.width1, nq = (n + 3) / 4;
+    const size_t row0 = (size_t)y * g.width1 * g.D;
+    uint32_t imask[M], tie[M][2];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int d = p * DPL + wta_pk_d<DPL, EV>(j, h);
+            tie[j][h] = (uint32_t)wta_tie(d, lanetie, 9);
+        }
+        const int d0 = p * DPL + wta_pk_d<DPL, EV>(j, 0), d1 = p * DPL + wta_pk_d<DPL, EV>(j, 1);
+        imask[j] = (lane_act && d0 < g.D ? 0u : 0xFFFFu) | (lane_act && d1 < g.D ? 0u : 0xFFFF0000u);
+    }
+    const int kq = 100 - g.uniq;
+    const float inv_kq = 1.0f / (float)kq;
+    const uint32_t Cc = (uint32_t)((32767 + NDIR * g.P2 + NDIR - 1) / NDIR);
+    const uint32_t Cc2 = Cc * 0x10001u;
+    const EvLayout el = evol_layout(g);
+    // buffer loads with 32-bit byte offsets off wave-uniform descriptors (one per volume slot and
+    // one for C'; the launcher's condition: every offset below 2^32), moved by a constant per
+    // iteration. Pixel 4q + r; past the last pixel group the loads read the next row or return 0
+    // past a range, and the results are never stored.
+    const uint32_t vbytes = (uint32_t)min(vol_elems * 2, (size_t)0xFFFFFFFFu);
+    __amdgpu_buffer_rsrc_t rsv[NDIR];
+#pragma unroll
+    for (int s = 0; s < NDIR; s++)
+        rsv[s] = __builtin_amdgcn_make_buffer_rsrc((void*)(vols + (size_t)s * vol_elems), 0, (int)vbytes, 0x00020000);
+    const uint32_t cbytes = (uint32_t)min((size_t)g.width1 * g.H * g.D * 2, (size_t)0xFFFFFFFFu);
+    const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((void*)Cv, 0, (int)cbytes, 0x00020000);
+    const uint32_t px0 = (uint32_t)y * (uint32_t)g.width1 + 4u * (uint32_t)w + (uint32_t)r;
+    uint32_t oc = (uint32_t)((row0 + (size_t)(4 * w + r) * g.D + dl) * 2);
+    uint32_t olo = EV ? px0 * el.ls + (uint32_t)dl : 0u, ohi = EV ? (uint32_t)el.hb + px0 * el.hs + (uint32_t)dl / 8 : 0u;
+    const uint32_t sc = 16u * (uint32_t)g.D * 2u, slo = 16u * el.ls, shi = 16u * el.hs;   // per iteration (4 groups)
+    auto load = [&](uint32_t (&c)[M], uint32_t (&v)[NDIR][NW]) {
+        bload_dw<M>(rsc, oc, c);
+        if constexpr (EV) {
+#pragma unroll
+            for (int s = 0; s < NDIR; s++) {
+                if constexpr (DPL == 8) {
+                    const auto t = __builtin_amdgcn_raw_buffer_load_b64(rsv[s], olo, 0, 0);
+                    v[s][0] = t[0]; v[s][1] = t[1];
+                    v[s][2] = __builtin_amdgcn_raw_buffer_load_b8(rsv[s], ohi, 0, 0);
+                } else {
+                    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rsv[s], olo, 0, 0);
+                    v[s][0] = t[0]; v[s][1] = t[1]; v[s][2] = t[2]; v[s][3] = t[3];
+                    v[s][4] = __builtin_amdgcn_raw_buffer_load_b16(rsv[s], ohi, 0, 0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NDIR; s++) bload_dw<M>(rsv[s], oc, v[s]);
+        }
+        oc += sc; olo += slo; ohi += shi;
+    };
+    uint32_t nc[M], nv[NDIR][NW];
+    load(nc, nv);
+    for (int q = w; q < nq; q += 4) {
+        uint32_t S2[M];
+        if constexpr (EV) {
+            // the NDIR deficits summed in the split order: low bytes through one perm per dword
+            // and half, bit 8 of the evens / odds spread to bytes by one multiply of the nibble
+            // (bit i -> bit 8i, the partial products' bits never overlap) and summed as bytes (<= 8)
+            uint32_t Alo[M], Hb[2 * NG];
+#pragma unroll
+            for (int j = 0; j < M; j++) Alo[j] = 0;
+#pragma unroll
+            for (int j = 0; j < 2 * NG; j++) Hb[j] = 0;
+#pragma unroll
+            for (int s = 0; s < NDIR; s++) {
+#pragma unroll
+                for (int gi = 0; gi < NG; gi++) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const uint32_t wd = nv[s][2 * gi + h];
+                        Alo[4 * gi + h] += __builtin_amdgcn_perm(0u, wd, 0x0C020C00u);       // (d 4h, d 4h + 2)
+                        Alo[4 * gi + 2 + h] += __builtin_amdgcn_perm(0u, wd, 0x0C030C01u);   // (d 4h + 1, d 4h + 3)
+                    }
+                    const uint32_t hb = (nv[s][DPL / 4] >> (8 * gi)) & 0xFFu;
+                    Hb[2 * gi] += ((hb & 0xFu) * 0x00204081u) & 0x01010101u;   // evens (4 bits: no carries)
+                    Hb[2 * gi + 1] += ((hb >> 4) * 0x00204081u) & 0x01010101u;  // odds
+                }
+            }
+#pragma unroll
+            for (int gi = 0; gi < NG; gi++) {
+                // C' of the group in the split order
+                const uint32_t c0 = nc[4 * gi], c1 = nc[4 * gi + 1], c2 = nc[4 * gi + 2], c3 = nc[4 * gi + 3];
+                const uint32_t Cs[4] = {__builtin_amdgcn_perm(c1, c0, 0x05040100u), __builtin_amdgcn_perm(c3, c2, 0x05040100u),
+                                        __builtin_amdgcn_perm(c1, c0, 0x07060302u), __builtin_amdgcn_perm(c3, c2, 0x07060302u)};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t hb2 = __builtin_amdgcn_perm(0u, Hb[2 * gi + (k >> 1)], (k & 1) ? 0x0C030C02u : 0x0C010C00u);
+                    const uint32_t E = Alo[4 * gi + k] + (hb2 << 8);
+                    const u16x2_t cm = __builtin_elementwise_min(as_v2(Cs[k]), as_v2(Cc2));
+                    const uint32_t s = as_u(cm * (u16x2_t){(unsigned short)NDIR, (unsigned short)NDIR} - as_v2(E));
+                    S2[4 * gi + k] = pk_min(s, 0x7FFF7FFFu) | imask[4 * gi + k];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                s16x2_t a = __builtin_bit_cast(s16x2_t, nv[0][j]);
+#pragma unroll
+                for (int s = 1; s < NDIR; s++) a = __builtin_elementwise_add_sat(a, __builtin_bit_cast(s16x2_t, nv[s][j]));
+                S2[j] = __builtin_bit_cast(uint32_t, a) | imask[j];
+            }
+        }
+        load(nc, nv);
+        uint32_t km = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < M; j++) {
+            const uint32_t klo = ((S2[j] & 0xFFFFu) << 9) | tie[j][0];
+            const uint32_t khi = ((S2[j] >> 7) & 0xFFFFFE00u) | tie[j][1];
+            km = min(km, min(klo, khi));
+        }
+        const uint32_t kmin = row_min_u32(km);
+        const int best = wta_untie((int)(kmin & 511u), lanetie, 9);
+        const int minS = (int)(kmin >> 9);
+#pragma unroll
+        for (int j = 0; j < M; j++) srow[p * M + j] = S2[j];
+        auto s_at = [&](uint32_t d) {                    // S of d from the pixel's LDS slice
+            const uint32_t k = d % DPL;
+            // EV: u16 index 2j + h of d's half in the split order
+            const uint32_t idx = EV ? 8 * (k >> 3) + 4 * (k & 1) + 2 * ((k >> 2) & 1) + ((k >> 1) & 1) : k;
+            // read as the u32 it was written as (a u16 view would be an aliasing violation)
+            return (int)((srow[(d / DPL) * M + idx / 2] >> (16 * (idx & 1))) & 0xFFFFu);
+        };
+        const int sm = s_at((uint32_t)max(best - 1, 0)), sp = s_at((uint32_t)min(best + 1, g.D - 1));
+        // uniqueness: S * kq < minS * 100 <=> S < T = ceil(minS * 100 / kq) (the quotient from the
+        // float reciprocal, then one correction each way; T clamped to 32768 > every real S). Some d
+        // outside {best - 1, best, best + 1} qualifies iff the sum of max(T - S, 0) over the pixel
+        // exceeds the window's share (census wta_pix16's test; d >= D hold 0xFFFF: no share)
+        const int num = minS * 100 + kq - 1;
+        int T = (int)((float)num * inv_kq);
+        T += (T + 1) * kq <= num ? 1 : 0;
+        T -= T * kq > num ? 1 : 0;
+        T = min(T, 32768);
+        const uint32_t T2 = (uint32_t)T * 0x10001u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < M; j++) acc = __builtin_amdgcn_sad_u16(as_u(__builtin_elementwise_sub_sat(as_v2(T2), as_v2(S2[j]))), 0u, acc);
+        const int total = (int)row_sum_u32(acc);
+        const int win = max(T - minS, 0) + (best > 0 ? max(T - sm, 0) : 0) + (best < g.D - 1 ? max(T - sp, 0) : 0);
+        const bool rej = total > win || minS >= 32767;
+        // subpixel, branch-free (tdiv_rcp's C truncation with both corrections as selects)
+        const int den = max(sm + sp - 2 * minS, 1);
+        const bool use = g.subpix && best > 0 && best < g.D - 1;
+        const int sn = (sm - sp) * 16 + den, sd = 2 * den;
+        int sq = (int)__builtin_truncf((float)sn * __builtin_amdgcn_rcpf((float)sd));
+        const int sr = sn - sq * sd;
+        sq += sn >= 0 ? (sr >= sd ? 1 : (sr < 0 ? -1 : 0)) : (sr <= -sd ? -1 : (sr > 0 ? 1 : 0));
+        const int d16 = best * 16 + (use ? sq : 0) + g.minD * 16;
+        const int x1 = 4 * q + r;
+        const bool wr = p == 0 && x1 < n;
+        const int x = wr ? g.minX1 + x1 : g.W + lane;
+        R.bst[x] = (int16_t)(rej ? -1 : best);
+        R.mins[x] = (uint16_t)minS;
+        R.drow[(wr && !rej) ? x : g.W + lane] = (int16_t)d16;
+    }
+    row_finish(g, tid, 256, R.drow, R.bst, R.mins, R.key, (int16_t*)R.mins, out + (size_t)y * out_stride);
+}
+
 // WTA of the OCV modes for D > 512 (the node's cfg allows disparity ranges up to 2048):
 // one pixel per wave, 64 lanes x 16 disparities per chunk of 1024, chunks in turn. Pass 1
 // sums S (OpenCV's saturating order), keeps the key min over (S + 32768) * 2048 + d and
@@ -2251,6 +2474,18 @@ static void launch_ocv_wta_e(const int16_t* C, const void* vols, size_t cells, i
     const size_t vol_elems = ocv_vol_elems(cells, sizeof(VT));
     const size_t lds = (size_t)16 * 16 * DPL * 2 + RowLds::bytes(g.W);
     const VT* v = (const VT*)vols;
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 2 && DPL <= 16 && (!EV || DPL >= 8)) {
+        // the plain int16 regime, packed (k_ocv_wta16_pk; 32-bit buffer offsets: slots below 4 GB)
+        if (SGM_OCV_WTA_PK != 0 && g.uniq < 100 && vol_elems * 2 < (size_t)kBufDrop) {
+            if (ndir == 8)
+                hipLaunchKernelGGL((k_ocv_wta16_pk<DPL, 8, EV>), dim3(g.H), dim3(256), lds, st, (const int16_t*)v,
+                                   vol_elems, g, out, out_stride, C);
+            else
+                hipLaunchKernelGGL((k_ocv_wta16_pk<DPL, 5, EV>), dim3(g.H), dim3(256), lds, st, (const int16_t*)v,
+                                   vol_elems, g, out, out_stride, C);
+            return;
+        }
+    }
     if (ndir == 8)
         hipLaunchKernelGGL((k_ocv_wta16<DPL, 8, VT, SAT, EV>), dim3(g.H), dim3(256), lds, st, v, vol_elems, g, out,
                            out_stride, C);
@@ -2334,19 +2569,6 @@ __device__ __forceinline__ int line_sum_i32(int v)
         v = (int)sw[0] + (int)sw[1];
     }
     return v;
-}
-template <int N>
-__device__ __forceinline__ void load_dw(const int16_t* p, uint32_t (&w)[N])
-{
-    if constexpr (N == 1) w[0] = *(const uint32_t*)p;
-    else if constexpr (N == 2) { const uint2 t = *(const uint2*)p; w[0] = t.x; w[1] = t.y; }
-    else {
-#pragma unroll
-        for (int c = 0; c < N / 4; c++) {
-            const uint4 t = ((const uint4*)p)[c];
-            w[4 * c] = t.x; w[4 * c + 1] = t.y; w[4 * c + 2] = t.z; w[4 * c + 3] = t.w;
-        }
-    }
 }
 // The packed pairs of the lane's deficits (Geom::evol) from its raw loads: w[0 .. M/2) the byte
 // plane's dwords, w[M/2] the bit-plane bytes (DPL = 8 or 16)
