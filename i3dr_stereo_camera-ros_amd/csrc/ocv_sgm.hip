@@ -13,7 +13,8 @@
 //                    lines per wave (16 lanes each);
 //                    int16 storage of L and minL as OpenCV's CostType
 //   k_ocv_wta16      S = the sum of L in OpenCV's saturating order, 16 lanes per pixel, + the
-//                    shared disp2 / LR row code (k_ocv_wta64 for D > 512).
+//                    shared disp2 / LR row code (k_ocv_wta64 for D > 512); k_ocv_wta16_pk the
+//                    same in packed u16 pairs where no cost leaves int16.
 // Volumes: int16 while no path cost can leave int16; otherwise (Geom::wide, e.g. the shipped
 // 2448x2048 D=480 block-21 config) int32 path volumes, gated per frame by the cost kernel's
 // overflow flag ("OpenCV semantics targets").
