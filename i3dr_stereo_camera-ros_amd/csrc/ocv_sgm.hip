@@ -56,42 +56,71 @@ constexpr int kMaxCost = 32767;
 // bt (optional, the fused cost's input): the Birchfield-Tomasi intervals of both channels at x,
 // packed u | lo << 8 | hi << 16, from the prefiltered / raw values at x - 1, x, x + 1 computed in
 // the thread (what bt_lohi reads from the planes)
+// Four adjacent pixels per thread (round 5; was one, with ~15 byte loads each): the 8 source bytes
+// x0 - 2 .. x0 + 5 of the three rows feed the six prefiltered values x0 - 1 .. x0 + 4 (the BT
+// intervals need both neighbours), and the four pixels of each plane go out as one dword / dwordx4
+// store where the address is aligned (else byte / dword stores).
 __global__ __launch_bounds__(256) void k_ocv_prefilter(const uint8_t* __restrict__ L, const uint8_t* __restrict__ R,
                                                        size_t stride, int W, int H, int ftzero,
                                                        uint8_t* __restrict__ planes /* 4 x W x H */,
                                                        uint32_t* __restrict__ bt /* 4 x W x H, or null */)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (x >= W) return;
+    const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y;
+    if (x0 >= W) return;
     const int img = blockIdx.z;
     const uint8_t* src = img ? R : L;
     uint8_t* pf = planes + (size_t)(2 * img) * W * H;
     uint8_t* raw = planes + (size_t)(2 * img + 1) * W * H;
-    const size_t o = (size_t)y * W + x;
+    const size_t o = (size_t)y * W + x0;
     const uint8_t* r = src + (size_t)y * stride;
     const uint8_t* n = y > 0 ? r - stride : r;
     const uint8_t* s = y < H - 1 ? r + stride : r;
-    auto pfraw = [&](int xx, int& p, int& q) {           // columns 0 and W - 1 are ftzero
-        if (xx <= 0 || xx >= W - 1) { p = ftzero; q = ftzero; return; }
-        const int v = (r[xx + 1] - r[xx - 1]) * 2 + n[xx + 1] - n[xx - 1] + s[xx + 1] - s[xx - 1];
-        p = min(max(v, -ftzero), ftzero) + ftzero;
-        q = r[xx];
-    };
-    int p0, q0;
-    pfraw(x, p0, q0);
-    pf[o] = (uint8_t)p0;
-    raw[o] = (uint8_t)q0;
+    // source bytes x0 - 2 + i (clamped reads: the columns they reach outside [1, W - 2] are forced
+    // to ftzero below)
+    int cr[8], cn[8], cs[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int xx = min(max(x0 - 2 + i, 0), W - 1);
+        cr[i] = r[xx]; cn[i] = n[xx]; cs[i] = s[xx];
+    }
+    int p[6], q[6];                                      // columns x0 - 1 + j; 0 and W - 1 are ftzero
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const int xx = x0 - 1 + j;
+        const int v = (cr[j + 2] - cr[j]) * 2 + cn[j + 2] - cn[j] + cs[j + 2] - cs[j];
+        const bool edge = xx <= 0 || xx >= W - 1;
+        p[j] = edge ? ftzero : min(max(v, -ftzero), ftzero) + ftzero;
+        q[j] = edge ? ftzero : cr[j + 1];
+    }
+    const bool full = x0 + 3 < W && (((uintptr_t)(pf + o) | (uintptr_t)(raw + o)) & 3) == 0;
+    if (full) {
+        *(uint32_t*)(pf + o) = (uint32_t)p[1] | (uint32_t)p[2] << 8 | (uint32_t)p[3] << 16 | (uint32_t)p[4] << 24;
+        *(uint32_t*)(raw + o) = (uint32_t)q[1] | (uint32_t)q[2] << 8 | (uint32_t)q[3] << 16 | (uint32_t)q[4] << 24;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (x0 + k < W) { pf[o + k] = (uint8_t)p[k + 1]; raw[o + k] = (uint8_t)q[k + 1]; }
+    }
     if (!bt) return;
-    int pl = p0, ql = q0, pr = p0, qr = q0;
-    if (x > 0) pfraw(x - 1, pl, ql);
-    if (x < W - 1) pfraw(x + 1, pr, qr);
-    auto pack = [](int u, int a, int b) {                 // bt_lohi with neighbours a (x - 1), b (x + 1)
-        const int ul = (u + a) / 2, ur = (u + b) / 2;
+    // bt_lohi of pixel k with neighbours k - 1 and k + 1 (the frame's first / last column takes
+    // itself as the missing neighbour)
+    auto pack = [&](const int (&a)[6], int k) {
+        const int u = a[k + 1];
+        const int l = x0 + k > 0 ? a[k] : u, rr = x0 + k < W - 1 ? a[k + 2] : u;
+        const int ul = (u + l) / 2, ur = (u + rr) / 2;
         return (uint32_t)u | (uint32_t)min(min(ul, ur), u) << 8 | (uint32_t)max(max(ul, ur), u) << 16;
     };
     const size_t plane = (size_t)W * H;
-    bt[(size_t)(2 * img) * plane + o] = pack(p0, pl, pr);
-    bt[(size_t)(2 * img + 1) * plane + o] = pack(q0, ql, qr);
+    uint32_t* bp = bt + (size_t)(2 * img) * plane + o;
+    uint32_t* bq = bt + (size_t)(2 * img + 1) * plane + o;
+    if (x0 + 3 < W && (((uintptr_t)bp | (uintptr_t)bq) & 15) == 0) {
+        *(uint4*)bp = make_uint4(pack(p, 0), pack(p, 1), pack(p, 2), pack(p, 3));
+        *(uint4*)bq = make_uint4(pack(q, 0), pack(q, 1), pack(q, 2), pack(q, 3));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (x0 + k < W) { bp[k] = pack(p, k); bq[k] = pack(q, k); }
+    }
 }
 
 __device__ __forceinline__ void bt_lohi(const uint8_t* a, int x, int W, int& u, int& lo, int& hi)
@@ -2264,7 +2293,7 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
     const bool simd_only = g.wide == 1 && (g.compat & SGM_OCV_SIMD_SAT);
     const bool fused = ocv_cost_takes_fused(g);
     uint32_t* bt = fused ? (uint32_t*)(planes + ocv_planes_bytes(g.W, g.H)) : nullptr;
-    hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 255) / 256, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
+    hipLaunchKernelGGL(k_ocv_prefilter, dim3((g.W + 1023) / 1024, g.H, 2), dim3(256), 0, st, L, R, stride, g.W, g.H,
                        g.ftzero, planes, bt);
     const bool sat2 = g.wide && (g.compat & SGM_OCV_SIMD_SAT) && ocv_hsum_cannot_saturate(g) && lds <= 64 * 1024 &&
                       (size_t)(2 * g.SH2 + 1) * 256 * 4 <= 64 * 1024 && !std::getenv("SGM_OCV_SAT_SEQ");
