@@ -527,6 +527,7 @@ struct FuseGeo {
 struct FuseGrid {
     int strips, bands, chunks, band_rows, ncomp, total, per_xcd;
 };
+constexpr uint32_t kFuseDrop = 0x80000000u;      // a byte offset past every C' row descriptor's range
 // TRK: what the overflow flag tracks (ocv_fuse_track): 0 nothing (no gate), 1 the max of C' itself
 // (box + P2 below 2^16 whatever the pixels; P2 taken off at the end), 2 the max of C' - P2
 template <int R, int DPC, int I, int TRK>
@@ -779,18 +780,34 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             const __amdgpu_buffer_rsrc_t crow = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(C32 + (size_t)y * rowC), 0, (int)(rowC * 4), 0x00020000);
             const uint32_t vb = 4u * (uint32_t)(((x0 + xa) * gD + d0) / 2 + bp);
+            if constexpr (R <= SGM_FUSE_BUFST) {
+                // branch-free: an output past the segment's end goes to an offset past the range,
+                // where the hardware drops it, and the flag's max is a select (1080p block 5 cost
+                // 0.210 -> 0.204 ms; at R = 21 the same form measured 2.00 against 1.97 for the
+                // branches below, and the branches with descriptor stores 2.02: profiles/
+                // r05_ocv_cost_box_ab.jsonl, r05_ocv_cost_box2_ab.jsonl)
+                const int nj = xb - xa;                      // outputs of the segment (> 0)
+                const bool skip0 = col0 && xa == 0 && y > 0; // COL0_LEGACY's column: not in the flag
 #pragma unroll
-            for (int j = 0; j < L; j++) {
-                if (j > 0) sum += w[j + R - 1] - w[j - 1];
-                if (xa + j < xb) {
-                    if constexpr (TRK != 0)
-                        if (!(col0 && xa + j == 0 && y > 0))
-                            bmax = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
-                    if constexpr (R <= SGM_FUSE_BUFST)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), crow, (int)vb,
-                                                              j * gD * 2, 0);
-                    else
-                        C32[ob + (uint32_t)(j * (gD / 2))] = __builtin_bit_cast(uint32_t, sum);
+                for (int j = 0; j < L; j++) {
+                    if (j > 0) sum += w[j + R - 1] - w[j - 1];
+                    const bool ok = j < nj;
+                    if constexpr (TRK != 0) {
+                        const u16x2_t cand = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
+                        bmax = (ok && !(j == 0 && skip0)) ? cand : bmax;
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b32(as_u(sum), crow, ok ? (int)vb : (int)kFuseDrop, j * gD * 2, 0);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < L; j++) {
+                    if (j > 0) sum += w[j + R - 1] - w[j - 1];
+                    if (xa + j < xb) {
+                        if constexpr (TRK != 0)
+                            if (!(col0 && xa + j == 0 && y > 0))
+                                bmax = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
+                        C32[ob + (uint32_t)(j * (gD / 2))] = as_u(sum);
+                    }
                 }
             }
             if (tail) {                                      // OpenCV's bottom rows: never recomputed
@@ -803,7 +820,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
 #pragma unroll
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
-                    const uint32_t c = fullDP ? gP2 * 0x10001u : __builtin_bit_cast(uint32_t, sum);
+                    const uint32_t c = fullDP ? gP2 * 0x10001u : as_u(sum);
                     if (xa + j < xb)
                         for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
                     o += gD / 2;
