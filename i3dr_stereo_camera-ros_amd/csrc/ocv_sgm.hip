@@ -1366,16 +1366,16 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // direction that start together run together
     int b = blockIdx.x, dir = 0, slot = 0;
     if (ilv) {
-        int nact = 0;
+        int nact = 0, nbd = 0;
         for (int i = 0; i < 8; i++) nact += nb[i] > 0;
         const int k = b % nact;
         b /= nact;
         for (int i = 0, c = 0; i < 8; i++) {
             if (!((dirmask >> i) & 1)) continue;
-            if (nb[i] > 0 && c++ == k) { dir = i; break; }
+            if (nb[i] > 0 && c++ == k) { dir = i; nbd = nb[i]; break; }
             slot++;
         }
-        if (b >= nb[dir]) return;
+        if (b >= nbd) return;
     } else {
         for (int i = 0; i < 8; i++) {
             if (!((dirmask >> i) & 1)) continue;
@@ -1384,6 +1384,12 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             slot++;
         }
     }
+    // uniform by construction (block-level values); stated, so the volume's buffer descriptor
+    // stays in SGPRs (hipcc had lost track after the round-robin deal and wrapped every buffer
+    // load and store of the small-D instantiations in a readfirstlane waterfall loop)
+    dir = __builtin_amdgcn_readfirstlane(dir);
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    b = __builtin_amdgcn_readfirstlane(b);
     VT* V = vols + (size_t)slot * vol_elems;
     constexpr int NLW = 64 / LPL;                      // lines per wave
     constexpr bool kRaw = sizeof(VT) == 4;             // store the int path costs (Geom::wide)
