@@ -1,0 +1,80 @@
+"""Code-generation guards on the built libsgm_hip.so (CPU only: the gfx950 code objects are read
+out of the library's .hip_fatbin section and disassembled with the ROCm LLVM tools).
+
+Round 5 found a silent regression that no parity test could see: after the round-robin deal of
+the path directions, hipcc no longer proved the block's volume slot uniform and wrapped every
+buffer load and store of the small-D `k_ocv_paths` instantiations in a readfirstlane waterfall
+loop (135 `v_readfirstlane_b32` per kernel; C1 paths 0.080 -> 0.101 ms). The kernel now states
+the values uniform; this test keeps it that way for every path-kernel instantiation and for the
+census path / fused kernels and the packed OCV WTA.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "i3dr_stereo_camera-ros_amd", "lib", "libsgm_hip.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _disassembly(tmp_path):
+    if not os.path.exists(LIB):
+        pytest.skip("libsgm_hip.so not built")
+    for tool in ("clang-offload-bundler", "llvm-objdump"):
+        if not os.path.exists(os.path.join(LLVM, tool)):
+            pytest.skip(f"{tool} not available")
+    objcopy = shutil.which("objcopy")
+    if not objcopy:
+        pytest.skip("objcopy not available")
+    fat = tmp_path / "fatbin"
+    subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", LIB], check=True, capture_output=True)
+    data = fat.read_bytes()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+    assert starts, "no offload bundle in .hip_fatbin"
+    text = []
+    for i, s in enumerate(starts):
+        part = tmp_path / f"b{i}"
+        part.write_bytes(data[s:starts[i + 1] if i + 1 < len(starts) else len(data)])
+        co = tmp_path / f"b{i}.co"
+        r = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+        if r.returncode != 0 or not co.exists() or co.stat().st_size == 0:
+            continue
+        d = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", str(co)],
+                           capture_output=True, text=True)
+        text.append(d.stdout)
+    return "\n".join(text)
+
+
+def _kernels(asm, prefix):
+    out = {}
+    for m in re.finditer(r"^[0-9a-f]+ <(" + re.escape(prefix) + r"\S*)>:\n", asm, re.M):
+        end = asm.find("\n\n", m.end())
+        out[m.group(1)] = asm[m.end():end if end > 0 else len(asm)]
+    return out
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    return _disassembly(tmp_path_factory.mktemp("isa"))
+
+
+def test_path_kernels_have_no_waterfall_loops(asm):
+    ks = _kernels(asm, "_ZN3sgm11k_ocv_paths")
+    assert len(ks) >= 30, f"expected every k_ocv_paths instantiation, found {len(ks)}"
+    for name, body in ks.items():
+        n = body.count("v_readfirstlane_b32")
+        assert n <= 16, f"{name}: {n} v_readfirstlane (a waterfall loop around non-uniform buffer descriptors?)"
+
+
+def test_census_and_wta_kernels_have_no_waterfall_loops(asm):
+    for prefix in ("_ZN3sgm16k_census_fused16", "_ZN3sgm16k_census_paths16", "_ZN3sgm14k_ocv_wta16_pk"):
+        ks = _kernels(asm, prefix)
+        assert ks, f"no {prefix} in the library"
+        for name, body in ks.items():
+            n = body.count("v_readfirstlane_b32")
+            assert n <= 16, f"{name}: {n} v_readfirstlane"
