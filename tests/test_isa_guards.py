@@ -30,8 +30,13 @@ def _disassembly(tmp_path):
     objcopy = shutil.which("objcopy")
     if not objcopy:
         pytest.skip("objcopy not available")
+    # objcopy rewrites its input when no output file is given: work on a copy, never on the
+    # library a test process may have mapped
+    lib = tmp_path / "lib.so"
+    shutil.copyfile(LIB, lib)
     fat = tmp_path / "fatbin"
-    subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", LIB], check=True, capture_output=True)
+    subprocess.run([objcopy, "--dump-section", f".hip_fatbin={fat}", str(lib), str(tmp_path / "lib_out.so")],
+                   check=True, capture_output=True)
     data = fat.read_bytes()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
     assert starts, "no offload bundle in .hip_fatbin"
