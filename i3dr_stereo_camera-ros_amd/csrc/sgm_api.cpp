@@ -487,13 +487,15 @@ int run_post(sgm_handle* h, const Layout& l, const Geom& g, int16_t* dOut, size_
 // profiles/r03_ocv_vwta_ab.jsonl, ms per frame off -> on: shipped 2448x2048 D=480 MODE_SGBM
 // 14.54 -> 13.93, MODE_HH 21.82 -> 21.63; 1080p D=128 MODE_SGBM 1.85 -> 2.11, MODE_HH 2.55 ->
 // 2.48; C1 0.23 -> 0.41). SGM_OCV_VWTA = 0 / 1 forces it off / on (parity tests run both).
-// MODE_HH with D <= 256 and uniqueness < 100 keeps the row WTA since it is packed
+// D <= 128 with uniqueness < 100 keeps the row WTA in both modes since it is packed
 // (k_ocv_wta16_pk, which also lets the paths write deficit volumes): 1080p D=128 MODE_HH
-// 2.25 -> 1.97 ms (profiles/r05_ocv_hh_vwta_ab.jsonl).
+// 2.25 -> 1.97 ms (profiles/r05_ocv_hh_vwta_ab.jsonl), 4096x3000 D=128 MODE_SGBM 9.49-9.65 ->
+// 8.63; at 4096x3000 D=256 MODE_HH the fused kernel stays ahead (28.3-28.6 against 30.0 ms,
+// profiles/r05_ocv_12mp_vwta_ab.jsonl), so wider ranges keep the thresholds below.
 bool ocv_vwta_on(const Geom& g, int fullDP)
 {
     if (const char* e = std::getenv("SGM_OCV_VWTA")) return std::atoi(e) != 0;
-    if (fullDP && g.D <= 256 && g.uniq < 100) return false;
+    if (g.D <= 128 && g.uniq < 100) return false;
     return (double)g.width1 * g.H * g.D >= (fullDP ? 2.0e8 : 1.0e9);
 }
 
