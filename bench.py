@@ -352,17 +352,47 @@ def c5_leg(args, world):
     return json.loads(lines[-1])
 
 
-def gather_shard(seeds, elapsed, distributed, busy=None):
-    """Per-rank record of the frame shard: the synthetic frame seeds each rank owned and its own
-    timed-region length (the line's value uses the MAX of these)."""
-    mine = {"seeds": list(seeds), "elapsed_s": round(elapsed, 6)}
+def device_identity(device=None, local_rank=0):
+    """Which physical device a rank ran on: HIP ordinal, PCI domain:bus:device and UUID (torch's
+    device properties), so an N-rank line shows N distinct GPUs. `device=None` (dry run, no HIP)
+    reports the rank's local ordinal only."""
+    if device is None:
+        return {"ordinal": local_rank, "pci": None, "uuid": None, "name": "dry run (no HIP)"}
+    import torch
+    pr = torch.cuda.get_device_properties(device)
+    pci = None
+    if hasattr(pr, "pci_bus_id"):
+        pci = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    uuid = str(getattr(pr, "uuid", "")) or None
+    return {"ordinal": int(device), "pci": pci, "uuid": uuid, "name": pr.name,
+            "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES"))}
+
+
+def distinct_devices(shard):
+    """Number of distinct physical devices in a shard record (PCI address + UUID; the ordinal
+    when neither is known)."""
+    keys = set()
+    for r in shard:
+        d = r.get("device") or {}
+        keys.add((d.get("pci"), d.get("uuid")) if (d.get("pci") or d.get("uuid")) else ("ordinal", d.get("ordinal")))
+    return len(keys)
+
+
+def gather_shard(seeds, elapsed, distributed, busy=None, device=None, group=None):
+    """Per-rank record of the frame shard: the synthetic frame seeds each rank owned, its own
+    timed-region length (the line's value uses the MAX of these), the device it ran on and the
+    world size it saw. Gathered over `group` (the CPU-side gloo group: no RCCL kernel)."""
+    mine = {"seeds": list(seeds), "elapsed_s": round(elapsed, 6), "device": device}
     if busy is not None:
         mine["busy_s"] = round(busy, 6)
     if not distributed:
+        mine["world_size"] = 1
         return [mine]
     import torch.distributed as dist
+    mine["world_size"] = dist.get_world_size()
+    mine["rank"] = dist.get_rank()
     objs = [None] * dist.get_world_size()
-    dist.all_gather_object(objs, mine)
+    dist.all_gather_object(objs, mine, group=group)
     return objs
 
 
@@ -385,14 +415,14 @@ def dry_main(args, world, rank):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed_max = max_over_ranks(elapsed)
-    shard = gather_shard(ids, elapsed, distributed, busy)
+    shard = gather_shard(ids, elapsed, distributed, busy, device_identity(None, rank))
     if rank == 0:
         frames_total = args.frames * args.steps * world
         print(json.dumps({"metric": METRIC, "value": round(frames_total / elapsed_max, 3), "unit": "pairs/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4), "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "dry run (no HIP work)",
-                          "elapsed_max_s": elapsed_max, "shard": shard,
+                          "elapsed_max_s": elapsed_max, "shard": shard, "distinct_devices": distinct_devices(shard),
                           "config": {"workload": "dry run", "parallelism": f"frame-shard x{world}"}}))
     if distributed:
         dist.barrier()
@@ -461,8 +491,13 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # waits outside the timed region (while rank 0 alone runs the single-frame / C5 / CPU legs,
+        # which drive every device) and the shard gather go over a CPU-side gloo group: a waiting
+        # rank then holds no spinning RCCL kernel on its device
+        wait_group = dist.new_group(backend="gloo")
     else:
         torch.cuda.set_device(0)
+        wait_group = None
     device = torch.cuda.current_device()
     pkg = ge.load_package()
 
@@ -471,7 +506,7 @@ def main():
         if rank == 0:
             c5 = run_c5(args, max(world, args.gpus), pkg, torch, device)
         if distributed:
-            dist.barrier()
+            dist.barrier(group=wait_group)
         if rank == 0:
             if args.c5_only:
                 print(json.dumps(c5))
@@ -558,7 +593,7 @@ def main():
     eng.set_profiling(False)
 
     elapsed_max = max_over_ranks(elapsed, None if args.share_device else device)
-    shard = gather_shard(ids, elapsed, distributed)
+    shard = gather_shard(ids, elapsed, distributed, device=device_identity(device), group=wait_group)
 
     # single-frame latency beside the batch throughput (BASELINE's C2 is quoted as a single
     # frame): one sgm_match_device per frame on resident buffers, HIP events on the stream
@@ -651,6 +686,7 @@ def main():
             "profiled_frames": n_prof,
             "single_frame": single,
             "shard": shard,
+            "distinct_devices": distinct_devices(shard),
         }
     eng.close()
     if rank == 0:
@@ -660,7 +696,9 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(res))
     if distributed:
-        dist.barrier()              # rank 0's single-frame / C5 / CPU legs end before the group does
+        # rank 0's single-frame / C5 / CPU legs end before the group does; the wait is on the gloo
+        # group, so devices 1..N-1 are idle while the C5 child tiles over them
+        dist.barrier(group=wait_group)
         dist.destroy_process_group()
 
 

@@ -1360,173 +1360,4 @@ hipError_t launch_census_rowfin(const WtaFrames& wf, const Geom& g, size_t out_s
     return hipGetLastError();
 }
 
-#ifdef SGM_EXPERIMENT_BUILD
-// ====================================================================================
-// Prototype of DESIGN §8.2 (VERDICT r4 "do this" #2): the three top-down directions of a
-// column strip in ONE workgroup, sharing each cell's Hamming cost, writing one u16 partial
-// sum S3 = L(dir 0) + L(dir 2) + L(dir 3) (2 B/cell instead of three u8 volumes, 3 B/cell).
-// TIMING-ONLY (experiment builds): a strip of SC = NCOL - 2G output columns carries G ghost
-// columns per side; the diagonal lines move one column per row through LDS (column c reads
-// column c -/+ 1's state of the previous row), and every G rows the ghost lanes reload their
-// state from the neighbouring strips' edge buffers and the edge lanes publish theirs — without
-// the flags an exact version needs (the neighbour may not have reached the row), so the work
-// and the traffic are the exact version's minus its waits: an optimistic bound, compared with
-// the same three directions of k_census_paths16 on the same codes (sgm_exp_strip3).
-// Lane (c, p): column x0 - G + c, disparities p * DPL .. + DPL - 1 (16 lanes per column).
-template <int DPL, int NCOL>
-__global__ __launch_bounds__(NCOL * 16) void k_strip3_proto(const uint64_t* __restrict__ cL,
-                                                            const uint64_t* __restrict__ cR, Geom g, int G,
-                                                            uint32_t* __restrict__ S3, uint32_t* __restrict__ edge)
-{
-    constexpr int M = DPL / 2, NT = NCOL * 16;
-    extern __shared__ uint64_t lds_s3[];
-    const int tid = threadIdx.x, c = tid >> 4, p = tid & 15;
-    const int SC = NCOL - 2 * G;
-    const int x0 = g.minX1 + (int)blockIdx.x * SC;
-    const int x = x0 - G + c;
-    const int D = g.D, NSEG = NCOL + D - 1, NPAD = NSEG + NSEG / 16 + 1;
-    const int CB = NCOL + NPAD;                           // codes per staging buffer
-    uint32_t* xs = (uint32_t*)(lds_s3 + 2 * CB);          // [2 parities][2 dirs][M][NT] states
-    auto xsw = [&](int par, int dir, int i) -> uint32_t& { return xs[((par * 2 + dir) * M + i) * NT + tid]; };
-    auto xsr = [&](int par, int dir, int i, int t) -> uint32_t { return xs[((par * 2 + dir) * M + i) * NT + t]; };
-    const int xlo = x0 - G - g.minD - (D - 1);            // right code of segment entry 0
-    // staging: thread t < NCOL the left code of column t, t < NCOL + NSEG right entry t - NCOL
-    const bool sl = tid < NCOL, sr = !sl && tid < NCOL + NSEG;
-    const int sx = sl ? x0 - G + tid : xlo + (tid - NCOL);
-    const int sxc = min(max(sx, 0), g.W - 1);
-    const int sat = sl ? tid : NCOL + (tid - NCOL) + ((tid - NCOL) >> 4);
-    auto ld = [&](int y) -> uint64_t { return (sl || sr) ? (sl ? cL : cR)[(size_t)y * g.W + sxc] : 0; };
-    auto stg = [&](int par, uint64_t v) { if (sl || sr) lds_s3[par * CB + sat] = v; };
-    uint32_t imask[M], start[M];
-    make_imask<DPL, true>(p, D, imask, start);
-    const uint32_t P1P1 = (uint32_t)g.P1 * 0x10001u, P2P2 = ((uint32_t)g.P2 + kBaseP) * 0x10001u;
-    uint32_t Ld[M], Le[M], Lw[M];
-#pragma unroll
-    for (int i = 0; i < M; i++) { Ld[i] = start[i]; Le[i] = start[i]; Lw[i] = start[i]; }
-    uint64_t A = ld(0);
-    stg(0, A);
-    A = ld(min(1, g.H - 1));
-    uint64_t B = ld(min(2, g.H - 1));
-#pragma unroll
-    for (int i = 0; i < M; i++) { xsw(1, 0, i) = start[i]; xsw(1, 1, i) = start[i]; }
-    __syncthreads();
-    const bool central = c >= G && c < G + SC && x < g.maxX1;
-    uint32_t* const orow0 = S3 + ((size_t)(x - g.minX1) * D + p * DPL) / 2;
-    const int e0 = c + D - 1 - p * DPL;                  // segment entry of d = p * DPL
-    for (int y = 0; y < g.H; y++) {
-        const int par = y & 1;
-        const uint64_t* cb = lds_s3 + par * CB;
-        const uint64_t cl = cb[c];
-        // the cost of the lane's cells, once for the three directions
-        uint32_t C[M];
-#pragma unroll
-        for (int i = 0; i < M; i++) {
-            const int ea = e0 - 2 * i, eb = e0 - 2 * i - 1;
-            const uint64_t ra = cb[NCOL + ea + (ea >> 4)], rb = cb[NCOL + eb + (eb >> 4)];
-            C[i] = ham_acc(cl, ra, 0u) + (ham_acc(cl, rb, 0u) << 16);
-        }
-        // the diagonals' previous-row states: column c - 1 (dir 2) and c + 1 (dir 3)
-#pragma unroll
-        for (int i = 0; i < M; i++) {
-            Le[i] = xsr(par ^ 1, 0, i, max(tid - 16, 0));
-            Lw[i] = xsr(par ^ 1, 1, i, min(tid + 16, NT - 1));
-        }
-        if (G > 0 && y > 0 && y % G == 0) {               // ghost refresh (no flags: timing only)
-            const int nb = gridDim.x;
-            if (c < G && blockIdx.x > 0) {
-#pragma unroll
-                for (int i = 0; i < M; i++) Le[i] = edge[(((size_t)(blockIdx.x - 1) * 2 + 1) * M + i) * (16 * G) + (c * 16 + p)];
-            }
-            if (c >= NCOL - G && (int)blockIdx.x + 1 < nb) {
-#pragma unroll
-                for (int i = 0; i < M; i++)
-                    Lw[i] = edge[(((size_t)(blockIdx.x + 1) * 2 + 0) * M + i) * (16 * G) + ((c - (NCOL - G)) * 16 + p)];
-            }
-        }
-        uint32_t Ad[M], Ae[M], Aw[M];
-        auto rec = [&](uint32_t (&Lr)[M], uint32_t (&Labs)[M]) {
-            uint32_t q[M];
-#pragma unroll
-            for (int i = 0; i < M; i++) q[i] = Lr[i] + P1P1;
-            const uint32_t X = row_shr_n<1>(q[M - 1], kInfP2), Y = row_shl_n<1>(q[0], kInfP2);
-            uint32_t Op = alignbit16(q[0], X);
-#pragma unroll
-            for (int i = 0; i < M; i++) {
-                const uint32_t On = (i + 1 < M) ? alignbit16(q[i + 1], q[i]) : alignbit16(Y, q[M - 1]);
-                Labs[i] = pk_min(pk_min3_p(Op, On, Lr[i]), P2P2) + C[i];
-                Op = On;
-            }
-            p16_relative<DPL, 16>(Labs, Lr);
-        };
-        rec(Ld, Ad);
-        rec(Le, Ae);
-        rec(Lw, Aw);
-#pragma unroll
-        for (int i = 0; i < M; i++) { xsw(par, 0, i) = Le[i]; xsw(par, 1, i) = Lw[i]; }
-        if (G > 0 && y % G == G - 1) {                    // publish the edge states for the neighbours
-            if (c >= SC && c < SC + G) {
-#pragma unroll
-                for (int i = 0; i < M; i++) edge[(((size_t)blockIdx.x * 2 + 1) * M + i) * (16 * G) + ((c - SC) * 16 + p)] = Le[i];
-            }
-            if (c >= G && c < 2 * G) {
-#pragma unroll
-                for (int i = 0; i < M; i++) edge[(((size_t)blockIdx.x * 2 + 0) * M + i) * (16 * G) + ((c - G) * 16 + p)] = Lw[i];
-            }
-        }
-        if (central) {                                    // S3 = the three path costs (u16 pairs)
-            uint32_t o[M];
-#pragma unroll
-            for (int i = 0; i < M; i++) o[i] = (Ad[i] - kBaseP2) + (Ae[i] - kBaseP2) + (Aw[i] - kBaseP2);
-            uint32_t* dst = orow0 + (size_t)y * g.width1 * D / 2;
-#pragma unroll
-            for (int i = 0; i < M; i += 4) {
-                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-                __builtin_nontemporal_store((v4u){o[i], o[i + 1], o[i + 2], o[i + 3]}, (v4u*)(dst + i));
-            }
-        }
-        stg(par ^ 1, A);
-        A = B;
-        B = ld(min(y + 3, g.H - 1));
-        __syncthreads();
-    }
-}
-
-template <int DPL, int NCOL>
-static size_t strip3_lds(int D)
-{
-    const int NSEG = NCOL + D - 1, NPAD = NSEG + NSEG / 16 + 1;
-    return (size_t)2 * (NCOL + NPAD) * 8 + (size_t)2 * 2 * (DPL / 2) * NCOL * 16 * 4;
-}
-
-template <int DPL, int NC>
-static hipError_t strip3_go(const uint64_t* cL, const uint64_t* cR, const Geom& g, int G, uint32_t* S3, uint32_t* edge,
-                            hipStream_t st)
-{
-    const int SC = NC - 2 * G;
-    const size_t lds = strip3_lds<DPL, NC>(g.D);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_strip3_proto<DPL, NC>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_strip3_proto<DPL, NC>), dim3((g.width1 + SC - 1) / SC), dim3(NC * 16), lds, st, cL, cR, g, G,
-                       S3, edge);
-    return hipGetLastError();
-}
-
-// grid = strips of ncol - 2G columns; edge: 2 * strips * DPL/2 * 16 * G u32
-hipError_t launch_strip3_proto(const uint64_t* cL, const uint64_t* cR, const Geom& g, int ncol, int G, uint32_t* S3,
-                               uint32_t* edge, hipStream_t st)
-{
-    if (ncol - 2 * G <= 0) return hipErrorInvalidValue;
-    if (g.D == 128) {
-        if (ncol == 32) return strip3_go<8, 32>(cL, cR, g, G, S3, edge, st);
-        if (ncol == 48) return strip3_go<8, 48>(cL, cR, g, G, S3, edge, st);
-        if (ncol == 64) return strip3_go<8, 64>(cL, cR, g, G, S3, edge, st);
-    } else if (g.D == 256) {
-        if (ncol == 32) return strip3_go<16, 32>(cL, cR, g, G, S3, edge, st);
-        if (ncol == 48) return strip3_go<16, 48>(cL, cR, g, G, S3, edge, st);
-        if (ncol == 64) return strip3_go<16, 64>(cL, cR, g, G, S3, edge, st);
-    }
-    return hipErrorInvalidValue;
-}
-#endif  // SGM_EXPERIMENT_BUILD
-
 }  // namespace sgm

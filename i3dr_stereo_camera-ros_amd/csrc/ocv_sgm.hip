@@ -2384,7 +2384,7 @@ hipError_t launch_ocv_cost(const uint8_t* L, const uint8_t* R, size_t stride, co
 // vols: the direction volumes (vol_elems apart) followed by >= 64 * 32 VT of trash slots
 // skipdir >= 0: that direction keeps its volume slot but launches no blocks (k_ocv_vwta runs it)
 template <int DPL, int LPL, typename VT, bool SAT>
-static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, const Geom& g, int dirmask,
+static hipError_t launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, const Geom& g, int dirmask,
                                hipStream_t st, int skipdir)
 {
     VT* vols = (VT*)vols_;
@@ -2416,22 +2416,32 @@ static void launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells, cons
     const int use_buf = (size_t)g.width1 * g.H * g.D * sizeof(VT) < (size_t)kBufDrop && !getenv("SGM_OCV_NO_BUF");
     // packed u16 recurrence: the plain int16 regime with P1, P2 <= 32768 (SGM_OCV_PK=0 at build time: ints)
     const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
+    // the plain kernel writes deficit records only on its packed branch (8 or 16 values per lane,
+    // buffer offsets); ocv_evol_mode decided g.evol from the same conditions, and the WTA reads
+    // deficits whenever it is set: refuse a frame where the two disagree rather than hand the WTA
+    // int16 L volumes it would read as deficits (flagged kernels ignore evol and write full volumes)
+    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_buf && use_pk))
+        return hipErrorInvalidValue;
     if (total > 0)
         hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf, use_pk, ilv);
+    return hipSuccess;
 }
 
 // the plain kernels (wide != 1) and the flagged ones (wide != 0): int32 volumes for the scalar
 // branch, saturating int16 over the SIMD cost (Csat) for SIMD_SAT; with wide == 2 the one not
 // matching the frame's flag exits at once
 template <int DPL, int LPL>
-static void launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
-                               int dirmask, hipStream_t st, int skipdir)
+static hipError_t launch_ocv_paths_v(const int16_t* C, const int16_t* Csat, void* vols, size_t cells, const Geom& g,
+                                     int dirmask, hipStream_t st, int skipdir)
 {
-    if (g.wide != 1) launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st, skipdir);
-    if (g.wide == 0) return;
-    if (g.compat & SGM_OCV_SIMD_SAT) launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st, skipdir);
-    else launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st, skipdir);
+    if (g.wide != 1) {
+        const hipError_t e = launch_ocv_paths_l<DPL, LPL, int16_t, false>(C, vols, cells, g, dirmask, st, skipdir);
+        if (e != hipSuccess) return e;
+    }
+    if (g.wide == 0) return hipSuccess;
+    if (g.compat & SGM_OCV_SIMD_SAT) return launch_ocv_paths_l<DPL, LPL, int16_t, true>(Csat, vols, cells, g, dirmask, st, skipdir);
+    return launch_ocv_paths_l<DPL, LPL, int32_t, false>(C, vols, cells, g, dirmask, st, skipdir);
 }
 
 // Lanes per path line. A line is a sequential walk, so a launch with few lines is bound by
@@ -2498,26 +2508,27 @@ hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, s
                             int dirmask, hipStream_t st, int skipdir)
 {
     const int D = g.D;
+    hipError_t e = hipSuccess;
     const int lpl = ocv_lanes_per_line(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
     if (lpl == 64) {
-        if (D <= 512) launch_ocv_paths_v<8, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
-        else if (D <= 1024) launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
-        else launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        if (D <= 512) e = launch_ocv_paths_v<8, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 1024) e = launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else e = launch_ocv_paths_v<32, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
     } else if (lpl == 32) {
-        if (D <= 64) launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
-        else if (D <= 128) launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
-        else if (D <= 256) launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
-        else launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        if (D <= 64) e = launch_ocv_paths_v<2, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 128) e = launch_ocv_paths_v<4, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else if (D <= 256) e = launch_ocv_paths_v<8, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
+        else e = launch_ocv_paths_v<16, 32>(C, Csat, vols, cells, g, dirmask, st, skipdir);
     } else {
         switch (dpl_for(D)) {
-        case 1: launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
-        case 2: launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
-        case 4: launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
-        case 8: launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
-        default: launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;   // D <= 256 here
+        case 1: e = launch_ocv_paths_v<1, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 2: e = launch_ocv_paths_v<2, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 4: e = launch_ocv_paths_v<4, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        case 8: e = launch_ocv_paths_v<8, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;
+        default: e = launch_ocv_paths_v<16, 16>(C, Csat, vols, cells, g, dirmask, st, skipdir); break;   // D <= 256 here
         }
     }
-    return hipGetLastError();
+    return e != hipSuccess ? e : hipGetLastError();
 }
 
 template <int DPL, typename VT, bool SAT, bool EV>

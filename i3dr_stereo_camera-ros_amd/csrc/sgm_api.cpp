@@ -39,9 +39,6 @@ hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
-#ifdef SGM_EXPERIMENT_BUILD
-hipError_t launch_strip3_proto(const uint64_t*, const uint64_t*, const Geom&, int, int, uint32_t*, uint32_t*, hipStream_t);
-#endif
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -1049,17 +1046,15 @@ int sgm_host_unregister(sgm_handle* h, void* ptr)
     if (!h) return SGM_ERR_ARG;
     if (!ptr) return fail(h, SGM_ERR_ARG, "null host pointer");
     HIP_TRY(hipSetDevice(h->device), "hipSetDevice");
-    {
-        std::lock_guard<std::mutex> lk(h->mu);
-        if (h->done_stream) HIP_TRY(hipEventSynchronize(h->done), "hipEventSynchronize");   // no kernel still writes it
-        for (size_t i = 0; i < h->regs.size(); i++)
-            if (h->regs[i].host == (char*)ptr) { h->regs.erase(h->regs.begin() + i); break; }
-    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->done_stream) HIP_TRY(hipEventSynchronize(h->done), "hipEventSynchronize");   // no kernel still writes it
     const hipError_t e = hipHostUnregister(ptr);
-    if (e != hipSuccess) {
+    if (e != hipSuccess) {                 // still registered: the handle keeps its mapping
         (void)hipGetLastError();
         return hip_fail(h, e, "hipHostUnregister");
     }
+    for (size_t i = 0; i < h->regs.size(); i++)
+        if (h->regs[i].host == (char*)ptr) { h->regs.erase(h->regs.begin() + i); break; }
     return SGM_OK;
 }
 
@@ -1677,26 +1672,31 @@ int sgm_match_tiled(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
 
 }  // extern "C"
 
-static void enable_peer_pair(int a, int b);
+static bool enable_peer_pair(int a, int b);
 
 // Overlap tile mode on device buffers (the C5 frame already in HBM of h's device): band b's
 // rows + halo go device -> devices[b % n] (xGMI peer copy), are matched there by
 // sgm_match_device on that device's sub-handle, and the band's own rows come back into
 // d_disp. Each device's bands run on its own host thread and stream.
 static int tiled_copy(void* dst, int ddev, size_t dpitch, const void* src, int sdev, size_t spitch, size_t width,
-                      size_t rows, hipStream_t st)
+                      size_t rows, bool peer_ok, hipStream_t st)
 {
     if (ddev != sdev && dpitch == width && spitch == width) {      // contiguous rows: one peer copy
         const hipError_t e = hipMemcpyPeerAsync(dst, ddev, src, sdev, width * rows, st);
         return e == hipSuccess ? 0 : (int)e;
     }
-    // strided rows (or one device): one 2-D copy over the unified address space, the same call
-    // within a device and between peers (the launcher enabled peer access between the pair)
-    const hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDefault, st);
-    if (e == hipSuccess) return 0;
-    if (ddev == sdev) return (int)e;
-    (void)hipGetLastError();
-    for (size_t r = 0; r < rows; r++) {       // a runtime that refuses the peer 2-D copy: one copy per row
+    // strided rows within a device, or between devices whose peer access is confirmed both ways
+    // (enable_peer_pair): one 2-D copy over the unified address space. Peer copies between
+    // devices without peer mappings take one hipMemcpyPeerAsync per row (the runtime stages them).
+    // (Between distinct physical devices this path has not run on hardware: the leased boxes have
+    // one GPU)
+    if (ddev == sdev || peer_ok) {
+        const hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDefault, st);
+        if (e == hipSuccess) return 0;
+        if (ddev == sdev) return (int)e;
+        (void)hipGetLastError();
+    }
+    for (size_t r = 0; r < rows; r++) {
         const hipError_t e2 = hipMemcpyPeerAsync((char*)dst + r * dpitch, ddev, (const char*)src + r * spitch, sdev,
                                                  width, st);
         if (e2 != hipSuccess) return (int)e2;
@@ -1723,7 +1723,8 @@ extern "C" int sgm_match_tiled_device(sgm_handle* h, const uint8_t* dL, const ui
         if (stream) HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize caller");
         if (h->done_stream) HIP_TRY(hipEventSynchronize(h->done), "hipEventSynchronize");
     }
-    for (int d : devs) enable_peer_pair(d, h->device);
+    std::vector<char> peer_ok(devs.size(), 0);           // peer access confirmed both ways
+    for (size_t i = 0; i < devs.size(); i++) peer_ok[i] = enable_peer_pair(devs[i], h->device) ? 1 : 0;
     const int nd = (int)devs.size(), hdev = h->device;
     return run_on_subs(h, devs, [&](int t, sgm_handle* sub) {
         for (int b = t; b < n_bands; b += nd) {
@@ -1742,12 +1743,13 @@ extern "C" int sgm_match_tiled_device(sgm_handle* h, const uint8_t* dL, const ui
             uint8_t* bl = (uint8_t*)sub->io_dev;
             uint8_t* br = bl + img;
             int16_t* bo = (int16_t*)(br + img);
-            if ((r = tiled_copy(bl, sub->device, W, dL + (size_t)e0 * stride, hdev, stride, W, He, sub->stream)) ||
-                (r = tiled_copy(br, sub->device, W, dR + (size_t)e0 * stride, hdev, stride, W, He, sub->stream)))
+            const bool pk = peer_ok[t] != 0;
+            if ((r = tiled_copy(bl, sub->device, W, dL + (size_t)e0 * stride, hdev, stride, W, He, pk, sub->stream)) ||
+                (r = tiled_copy(br, sub->device, W, dR + (size_t)e0 * stride, hdev, stride, W, He, pk, sub->stream)))
                 return fail(sub, SGM_ERR_DEVICE, std::string("band input copy: ") + hipGetErrorString((hipError_t)r));
             if ((r = sgm_match_device(sub, bl, br, W, He, W, bo, W, nullptr))) return r;
             if ((r = tiled_copy(dOut + (size_t)c0 * out_stride, hdev, out_stride * 2, bo + (size_t)(c0 - e0) * W,
-                                sub->device, (size_t)W * 2, (size_t)W * 2, c1 - c0, sub->stream)))
+                                sub->device, (size_t)W * 2, (size_t)W * 2, c1 - c0, pk, sub->stream)))
                 return fail(sub, SGM_ERR_DEVICE, std::string("band output copy: ") + hipGetErrorString((hipError_t)r));
             if (hipStreamSynchronize(sub->stream) != hipSuccess) return fail(sub, SGM_ERR_DEVICE, "band stream");
         }
@@ -1808,14 +1810,25 @@ hipError_t copy_between(void* dst, int ddev, const void* src, int sdev, size_t n
                         : hipMemcpyPeerAsync(dst, ddev, src, sdev, n, st);
 }
 
-void enable_peer(int dev, int peer)
+// Enables dev -> peer access; true when it is in effect (enabled now or before, or dev == peer).
+bool enable_peer(int dev, int peer)
 {
-    if (dev == peer) return;
+    if (dev == peer) return true;
     int ok = 0;
-    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) return;
-    if (hipSetDevice(dev) != hipSuccess) return;
-    (void)hipDeviceEnablePeerAccess(peer, 0);    // already enabled: fine
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess || !ok) {
+        (void)hipGetLastError();
+        return false;
+    }
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
     (void)hipGetLastError();
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
 }
 
 // Stream 2 + events of a band handle; the three path work lists uploaded for g.
@@ -2077,7 +2090,11 @@ int run_tiled_exact(sgm_handle* h, const uint8_t* L, const uint8_t* R, int W, in
 
 }  // namespace
 
-static void enable_peer_pair(int a, int b) { enable_peer(a, b); enable_peer(b, a); }
+static bool enable_peer_pair(int a, int b)
+{
+    const bool ab = enable_peer(a, b), ba = enable_peer(b, a);
+    return ab && ba;
+}
 
 extern "C" {
 
@@ -2285,67 +2302,3 @@ int sgm_debug_speckle(sgm_handle* h, int16_t* disp, int W, int H, int new_val, i
 }
 
 }  // extern "C"
-
-#ifdef SGM_EXPERIMENT_BUILD
-// DESIGN §8.2 prototype A/B (experiment builds only, tools/strip3_ab.py): on the census codes of
-// one frame (h's census parameters), ms per launch averaged over `reps`, interleaved:
-// ms[0] the three top-down directions (0, 2, 3) of k_census_paths16 (three u8 volumes),
-// ms[1] k_strip3_proto with strips of ncol - 2G columns (one u16 partial-sum volume),
-// ms[2] all eight directions of k_census_paths16 (the single-frame paths launch).
-extern "C" int sgm_exp_strip3(sgm_handle* h, const uint8_t* dL, const uint8_t* dR, int W, int H, int ncol, int G,
-                              int reps, float* ms)
-{
-    if (!h || !ms || h->params.mode != SGM_MODE_CENSUS8) return SGM_ERR_ARG;
-    std::lock_guard<std::mutex> lk(h->mu);
-    Geom g;
-    Layout l;
-    int rc = prepare(h, W, H, false, g, l);
-    if (rc || (rc = order_after_last(h, h->stream))) return rc;
-    hipStream_t st = h->stream;
-    char* ws = (char*)h->ws.base;
-    uint64_t* cL = (uint64_t*)(ws + l.cL[0]);
-    uint64_t* cR = (uint64_t*)(ws + l.cR[0]);
-    uint8_t* vols = (uint8_t*)(ws + l.vols[0]);
-    HIP_TRY(sgm::launch_census(dL, dR, W, W, H, cL, cR, st), "census");
-    const uint32_t *it_down, *it_all;
-    const int n_down = path_items(h, l, g, 0x0Du, 1, st, &it_down);
-    if (n_down < 0) return n_down;
-    std::vector<uint32_t> down_copy(n_down);
-    HIP_TRY(hipMemcpyAsync(down_copy.data(), it_down, (size_t)n_down * 4, hipMemcpyDeviceToHost, st), "items");
-    HIP_TRY(hipStreamSynchronize(st), "sync");
-    uint32_t* items_down = nullptr;
-    HIP_TRY(hipMalloc(&items_down, (size_t)n_down * 4), "hipMalloc");
-    HIP_TRY(hipMemcpy(items_down, down_copy.data(), (size_t)n_down * 4, hipMemcpyHostToDevice), "items");
-    const int n_all = path_items(h, l, g, 0xFFu, 1, st, &it_all);
-    if (n_all < 0) return n_all;
-    const int strips = (g.width1 + (ncol - 2 * G) - 1) / std::max(ncol - 2 * G, 1);
-    uint32_t* edge = nullptr;
-    HIP_TRY(hipMalloc(&edge, (size_t)strips * 2 * (g.D / 32) * 16 * std::max(G, 1) * 4 + 4096), "hipMalloc");
-    uint32_t* S3 = (uint32_t*)(vols + 4 * l.vol_bytes);           // direction slots 4-5: unused here
-    sgm::PathFrames pf{};
-    pf.cL[0] = cL; pf.cR[0] = cR; pf.vols[0] = vols; pf.n = 1;
-    hipEvent_t e[2];
-    HIP_TRY(hipEventCreate(&e[0]), "ev");
-    HIP_TRY(hipEventCreate(&e[1]), "ev");
-    double acc[3] = {0, 0, 0};
-    for (int r = -1; r < reps; r++) {
-        for (int k = 0; k < 3; k++) {
-            HIP_TRY(hipEventRecord(e[0], st), "ev");
-            if (k == 0) HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items_down, n_down, st), "down");
-            else if (k == 1) HIP_TRY(sgm::launch_strip3_proto(cL, cR, g, ncol, G, S3, edge, st), "strip3");
-            else HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, it_all, n_all, st), "all");
-            HIP_TRY(hipEventRecord(e[1], st), "ev");
-            HIP_TRY(hipEventSynchronize(e[1]), "sync");
-            float t = 0;
-            HIP_TRY(hipEventElapsedTime(&t, e[0], e[1]), "elapsed");
-            if (r >= 0) acc[k] += t;
-        }
-    }
-    for (int k = 0; k < 3; k++) ms[k] = (float)(acc[k] / std::max(reps, 1));
-    (void)hipEventDestroy(e[0]);
-    (void)hipEventDestroy(e[1]);
-    (void)hipFree(edge);
-    (void)hipFree(items_down);
-    return mark_done(h, st);
-}
-#endif

@@ -113,8 +113,11 @@ void sgm_destroy(sgm_handle* h);
  * registered: a registered output of sgm_match / sgm_match_f32 is copied back by DMA without the
  * runtime's pageable staging, or — sgm_match_f32 in the census mode without median / speckles —
  * written by the WTA kernel itself as the rows finish. The caller must unregister a buffer
- * before freeing it (unregistering waits for the handle's last call); the MatcherHIPSGM adapter
- * registers its persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat.               */
+ * before freeing it (unregistering waits for the handle's last call; on failure the buffer stays
+ * registered and mapped). sgm_destroy unregisters every buffer still registered through the
+ * handle: HIP registrations are process-wide, so a caller that keeps using a buffer page-locked
+ * after destroying the handle registers it again. The MatcherHIPSGM adapter registers its
+ * persistent disparity_lr, matcherOpenCVSGBM.cpp:34's output Mat.                              */
 int  sgm_host_register(sgm_handle* h, void* ptr, size_t bytes);
 int  sgm_host_unregister(sgm_handle* h, void* ptr);
 

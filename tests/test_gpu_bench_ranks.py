@@ -39,3 +39,8 @@ def test_bench_two_ranks_on_one_device(config):
     assert res["ms_per_step"] == pytest.approx(el * 1e3 / 3, rel=1e-3)   # the MAX over ranks
     assert res["value"] == pytest.approx(4 * 3 * 2 / el, rel=1e-3)
     assert res["roofline"]["frac"] > 0.05 and res["single_frame"]["ms"] > 0
+    # the record names each rank's device (both on device 0 here) and the world size it saw
+    assert [r["world_size"] for r in shard] == [2, 2]
+    devs = [r["device"] for r in shard]
+    assert all(d["ordinal"] == 0 and (d["pci"] or d["uuid"]) for d in devs), devs
+    assert devs[0]["pci"] == devs[1]["pci"] and res["distinct_devices"] == 1

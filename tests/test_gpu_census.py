@@ -274,14 +274,35 @@ def test_tiled_overlap_mode_disagreement(engine, oracle, synth, pkg, bands, halo
     assert frac < {0: 0.1, 16: 0.01, 64: 0.001, 128: 0.001}[halo]
 
 
-def test_c5_tiled_vs_full_frame(engine, synth, pkg):
-    """BASELINE config C5 (4096x3000, D=512, 8-path + subpixel + LR): 8 row bands with a
-    128-row halo (the 8-GPU layout, run here on the visible devices) against the
-    single-device full frame (44 GB of path volumes, resident in HBM)."""
+@pytest.fixture(scope="module")
+def c5_case(synth, pkg, oracle):
+    """BASELINE config C5 (4096x3000, D=512, 8-path + subpixel + LR): the frame, its parameters
+    and the oracle's disparity (OpenMP over lines; ~20 s and ~11 GB of host RAM for S), computed
+    once for the C5 tests."""
     h, w, D = 3000, 4096, 512
     left, right, _ = synth.stereo_pair(h, w, 0, D, seed=5, with_truth=False)
-    engine.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D))
-    full = engine.match(left, right)
+    p = pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    return left, right, p, ref
+
+
+@pytest.mark.timeout(600)
+def test_c5_full_frame_vs_oracle(engine, c5_case):
+    """C5 on one device against the oracle, bit for bit: the 32-lane path lines,
+    5.5 GB direction volumes (64-bit offsets: where a 32-bit overflow was once found) and the
+    lone frame's WTA at full size."""
+    left, right, p, ref = c5_case
+    engine.set_params(p)
+    got = engine.match(left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    assert (ref != -16).mean() > 0.5
+
+
+def test_c5_tiled_vs_full_frame(engine, c5_case):
+    """C5: 8 row bands with a 128-row halo (the 8-GPU layout, run here on the visible devices)
+    against the full frame (the oracle's)."""
+    left, right, p, full = c5_case
+    engine.set_params(p)
     tiled = engine.match_tiled(left, right, 8, 128)
     frac = float((tiled != full).mean())
     print(f"C5 8 bands, halo 128: {100 * frac:.4f} % of pixels differ from the full frame")
@@ -384,13 +405,11 @@ def test_tiled_exact_no_disparity_window(engine, pkg):
     assert (got == -16).all()
 
 
-def test_c5_tiled_exact_vs_full_frame(engine, synth, pkg):
+def test_c5_tiled_exact_vs_full_frame(engine, c5_case):
     """BASELINE config C5 (4096x3000, D=512) in exact mode: 8 bands with boundary-row
-    exchange equal the single-device full frame at every pixel."""
-    h, w, D = 3000, 4096, 512
-    left, right, _ = synth.stereo_pair(h, w, 0, D, seed=5, with_truth=False)
-    engine.set_params(pkg.default_params(pkg.MODE_CENSUS8, num_disparities=D))
-    full = engine.match(left, right)
+    exchange equal the full frame (the oracle's) at every pixel."""
+    left, right, p, full = c5_case
+    engine.set_params(p)
     tiled = engine.match_tiled_exact(left, right, 8)
     assert np.array_equal(tiled, full), f"{(tiled != full).sum()} pixels differ"
 

@@ -7,6 +7,11 @@ The setters reach cv::StereoSGBM unchanged (matcherOpenCVSGBM.cpp:53-110, via
 generate_disparity.cpp:241-261). With a 21 x 21 box at ftzero 15 a cost may leave int16
 (bound 441 * 93 + 400 = 41 413), so the engine runs gated: the cost kernel flags the C'
 values that do, and only then do the int32 volumes run (Geom::wide == 2).
+
+The processing launch (launch/stereo_processing.launch:65-66, stereo_algorithm 1) keeps those
+values and searches minD 0, D 752 instead: D > 512 takes the full int16 path volumes (no 9-bit
+deficits), 64-bit offsets (a 5.2 GB volume is past the 32-bit buffer range) and 64-lane path
+lines with 16 values per lane whose last active lane straddles D (752 % 32 = 16).
 """
 import os
 
@@ -26,9 +31,17 @@ def _params(pkg, mode):
     return pkg.default_params(pkg.MODE_OCV_SGBM5 if mode == "sgbm" else pkg.MODE_OCV_HH8, **REF_KW)
 
 
+PROC_KW = dict(REF_KW, min_disparity=0, num_disparities=752)
+
+
 @pytest.fixture(scope="module")
 def ref_frame(synth):
     return synth.stereo_pair(REF_H, REF_W, 147, 480, seed=2448)
+
+
+@pytest.fixture(scope="module")
+def proc_frame(synth):
+    return synth.stereo_pair(REF_H, REF_W, 0, 752, seed=752)
 
 
 @pytest.mark.parametrize("mode", ["sgbm", "hh"])
@@ -137,3 +150,28 @@ def test_reference_config_hh_device_batch(engine, pkg, ref_frame, compat):
     for i in (0, n - 1):
         single = engine.match(ls[i], rs[i])
         assert np.array_equal(got[i], single), f"frame {i}: {(got[i] != single).sum()} pixels differ"
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_processing_config_full_frame_vs_oracle(engine, oracle, pkg, proc_frame, mode, monkeypatch):
+    """The processing launch's matcher (stereo_processing.launch:65-66: minD 0, D 752; block 21,
+    uniqueness 2, speckle 1000 / 4, cap 7, P1 200, P2 400 from stereo_matcher.launch:39-47) on a
+    whole 2448 x 2048 frame under the default melodic build, bit for bit against the oracle
+    (VERDICT r5 #1): five or eight full int16 volumes of 5.2 GB each, 64-bit path offsets, the
+    straddling lane, median and speckles; then the same frame with the int32 volumes forced
+    (SGM_OCV_GATE=0, 10.4 GB each) equals it. (The oracle takes 1-2 minutes per mode.)"""
+    left, right, truth = proc_frame
+    p = pkg.default_params(pkg.MODE_OCV_SGBM5 if mode == "sgbm" else pkg.MODE_OCV_HH8, **PROC_KW)
+    assert p.ocv_compat == pkg.COMPAT_MELODIC
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    valid = ref != -16
+    assert valid.mean() > 0.5
+    err = np.abs(ref[valid] / 16.0 - truth[valid])
+    assert np.median(err) < 0.5, np.median(err)
+    monkeypatch.setenv("SGM_OCV_GATE", "0")
+    got32 = engine.match(left, right)
+    assert np.array_equal(got32, ref), f"int32 volumes: {(got32 != ref).sum()} pixels differ"

@@ -8,7 +8,10 @@ speckle), 1920x1080 D=128 in MODE_SGBM / MODE_HH, and the reference's shipped SG
 config (launch/stereo_matcher.launch:37-48 at the capture size of stereo_capture.launch:14-15:
 2448x2048, minD 147, D 480, block 21, cap 7, uniqueness 2, speckle 1000/4, P1 200, P2 400)
 in MODE_SGBM / MODE_HH, gated (int16 volumes unless a cost leaves int16) and with the static
-int32 volumes (SGM_OCV_GATE=0). Per case: per-stage HIP-event times with each stage's
+int32 volumes (SGM_OCV_GATE=0), and the processing launch's SGBM search
+(launch/stereo_processing.launch:65-66: minD 0, D 752, the rest of stereo_matcher.launch:39-47) at
+the same size: D > 512, so full int16 volumes (no deficits), 64-bit path offsets and a 64-lane
+line whose lanes carry 16 values (752 % 32 = 16). Per case: per-stage HIP-event times with each stage's
 algorithmic bytes and fraction of the 8 TB/s HBM peak (the dominant stage is `roofline`).
 """
 import argparse
@@ -54,6 +57,9 @@ def main():
             tag = "gated" if gate == "1" else "int32 volumes"
             cases.append((f"refcfg 2448x2048 minD 147 D 480 block 21 {mname} ({tag})", 2048, 2448, mode,
                           dict(ref_kw, _gate=gate)))
+    for mname, mode in (("MODE_SGBM", pkg.MODE_OCV_SGBM5), ("MODE_HH", pkg.MODE_OCV_HH8)):
+        cases.append((f"proccfg 2448x2048 minD 0 D 752 block 21 {mname}", 2048, 2448, mode,
+                      dict(ref_kw, min_disparity=0, num_disparities=752)))
     eng = pkg.Engine(0)
     st = torch.cuda.Stream()
     for name, h, w, mode, kw in cases:
