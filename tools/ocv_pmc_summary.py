@@ -13,7 +13,7 @@ import sys
 def main():
     d = sys.argv[1]
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(f"{d}/pass*_counter_collection.csv"):
+    for f in glob.glob(f"{d}/**/pass*_counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
