@@ -1237,6 +1237,14 @@ __device__ __forceinline__ int line_min_i32(int v)
 // buffer offset of a dropped store: past every buffer range the buffer path is used for
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
+// a 64-bit value the caller knows to be wave-uniform, stated so (kept in SGPRs)
+__device__ __forceinline__ long long uni64(long long v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 #ifndef SGM_OCV_VWTA_PK
 #define SGM_OCV_VWTA_PK 1  // k_ocv_vwta_pk for the plain int16 regime with uniqueness < 100
 #endif
@@ -1321,8 +1329,8 @@ __device__ __forceinline__ void bload_dw(__amdgpu_buffer_rsrc_t rs, uint32_t off
 // planes: DPL low bytes at lo_off, DPL bits (evol_pos order) at hi_off; nontemporal, streamed once
 // into the WTA
 template <int DPL>
-__device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t lo_off, uint32_t hi_off,
-                                           const uint32_t (&E2)[DPL / 2])
+__device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t lo_off, __amdgpu_buffer_rsrc_t rsh,
+                                           uint32_t hi_off, const uint32_t (&E2)[DPL / 2])
 {
     static_assert(DPL == 8 || DPL == 16, "one or two groups of 8 deficits per lane");
     constexpr int NG = DPL / 8;
@@ -1340,10 +1348,10 @@ __device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t l
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     if constexpr (NG == 1) {
         __builtin_amdgcn_raw_buffer_store_b64((v2u){lo[0], lo[1]}, rs, lo_off, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)hb, rs, hi_off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)hb, rsh, hi_off, 0, 2);
     } else {
         __builtin_amdgcn_raw_buffer_store_b128((v4u){lo[0], lo[1], lo[2], lo[3]}, rs, lo_off, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)hb, rs, hi_off, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)hb, rsh, hi_off, 0, 2);
     }
 }
 
@@ -1435,7 +1443,16 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
     // Straight-line steps (no branch, so hipcc keeps counted vmcnt waits across the loop).
     // The first PF steps are peeled (pv = false only at step 0, a constant elsewhere).
     if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 2) {
-        if (use_buf && use_pk) {     // the plain int16 regime in packed u16 pairs (ocv_step_pk)
+        // the plain int16 regime in packed u16 pairs (ocv_step_pk): volumes below 4 GB with 32-bit
+        // buffer offsets that move by the step, or — 64-lane lines (one line per wave, so a step's
+        // cell is wave-uniform) — any size, each step's descriptors rebased on the step's cell
+        // (64-bit scalar arithmetic, lane offsets within the cell): the D > 512 frames (the
+        // processing launch's D = 752 has 5.2 GB int16 volumes) keep the packed step and the
+        // deficit records. Only 16 values per lane (512 < D <= 1024) take it: in the 8-value
+        // instantiation the per-step descriptors of 16 rows in flight cost SGPRs the buffer-offset
+        // form of the same kernel (the shipped D=480 config) would pay for (105 -> 138 VGPRs), and
+        // 32 values (D > 1024) have a lane straddling D that would load past its rebased cell.
+        if (use_pk && (use_buf || (LPL == 64 && DPL == 16))) {
             constexpr int M = DPL / 2;
             const size_t cells = (size_t)g.width1 * g.H * g.D;
             const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(uint32_t)(cells * 2), 0x00020000);
@@ -1458,14 +1475,28 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             const long long pix0 = (long long)ybase * g.width1 + x0, pstep = (long long)ry * g.width1 + rx;
             uint32_t ev_lo = (uint32_t)(pix0 * el.ls + dl), ev_hi = (uint32_t)(el.hb + pix0 * el.hs + dl / 8);
             const uint32_t ev_step = (uint32_t)(pstep * el.ls), ev_hstep = (uint32_t)(pstep * el.hs);
-            auto run = [&](auto evc) {
+            // rebased form (REB): the line's cell / pixel of step i (clamped to its last step, so every
+            // descriptor base stays inside the volume), stated wave-uniform
+            const long long ucb = uni64(cbase), ucs = uni64(cstep), upx = uni64(pix0), ups = uni64(pstep);
+            const int ulast = __builtin_amdgcn_readfirstlane(ilast);
+            const uint32_t cell_bytes = (uint32_t)g.D * 2u;
+            auto rs_cell = [&](const void* base, int i) {
+                return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (ucb + (long long)min(i, ulast) * ucs) * 2),
+                                                         0, (int)cell_bytes, 0x00020000);
+            };
+            auto run = [&](auto evc, auto rebc) {
                 constexpr bool EV = decltype(evc)::value;
+                constexpr bool REB = decltype(rebc)::value;
                 uint32_t C2[PF][M], L2[M];
 #pragma unroll
                 for (int i = 0; i < M; i++) L2[i] = 0;
                 uint32_t delta2 = P2 * 0x10001u;         // the path's first pixel: L = C - P2
+                auto loadC = [&](int i, uint32_t (&c)[M]) {
+                    if constexpr (REB) bload_dw<M>(rs_cell(C, i), (uint32_t)dl * 2u, c);
+                    else { bload_dw<M>(rsC, ld_b, c); ld_b += bstep; }
+                };
 #pragma unroll
-                for (int q = 0; q < PF; q++) { bload_dw<M>(rsC, ld_b, C2[q]); ld_b += bstep; }
+                for (int q = 0; q < PF; q++) loadC(q, C2[q]);
                 auto steps = [&](int i0) {
 #pragma unroll
                     for (int q = 0; q < PF; q++) {
@@ -1473,21 +1504,30 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                         uint32_t E2[M];
                         const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2[q], L2, delta2, P1P1, imask, p, EV ? E2 : nullptr);
                         const bool ok = lane_act && i < n;
-                        if constexpr (EV) {
-                            evol_store<DPL>(rsV, ok ? ev_lo : kBufDrop, ok ? ev_hi : kBufDrop, E2);
+                        if constexpr (EV && REB) {
+                            const long long px = upx + (long long)min(i, ulast) * ups;
+                            const auto rlo = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)V + px * el.ls), 0, (int)el.ls, 0x00020000);
+                            const auto rhi = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)V + el.hb + px * el.hs), 0,
+                                                                               (int)el.hs, 0x00020000);
+                            evol_store<DPL>(rlo, ok ? (uint32_t)dl : kBufDrop, rhi, ok ? (uint32_t)dl / 8u : kBufDrop, E2);
+                        } else if constexpr (EV) {
+                            evol_store<DPL>(rsV, ok ? ev_lo : kBufDrop, rsV, ok ? ev_hi : kBufDrop, E2);
                             ev_lo += ev_step;
                             ev_hi += ev_hstep;
-                        } else if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
-                            bstore_dw<8>(rsV, ok ? st_b : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
-                            bstore_dw<8>(rsV, ok && !straddle ? st_b + 32u : kBufDrop,
-                                         *reinterpret_cast<const uint32_t(*)[8]>(&L2[8]));
                         } else {
-                            bstore_dw<M>(rsV, ok ? st_b : kBufDrop, L2);
+                            const auto rsS = REB ? rs_cell(V, i) : rsV;
+                            const uint32_t so = REB ? (uint32_t)dl * 2u : st_b;
+                            if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
+                                bstore_dw<8>(rsS, ok ? so : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
+                                bstore_dw<8>(rsS, ok && !straddle ? so + 32u : kBufDrop,
+                                             *reinterpret_cast<const uint32_t(*)[8]>(&L2[8]));
+                            } else {
+                                bstore_dw<M>(rsS, ok ? so : kBufDrop, L2);
+                            }
                         }
                         delta2 = ((uint32_t)line_min_i32<LPL>((int)lmin) + P2) * 0x10001u;
-                        bload_dw<M>(rsC, ld_b, C2[q]);
+                        loadC(i + PF, C2[q]);
                         st_b += bstep;
-                        ld_b += bstep;
                     }
                 };
                 for (int i0 = 0; i0 < nmax; i0 += PF) {
@@ -1495,13 +1535,25 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                     steps(i0);
                 }
             };
-            if constexpr (DPL == 8 || DPL == 16) {
-                if (g.evol) {
-                    run(std::true_type{});
+            if constexpr (LPL == 64 && DPL == 16) {
+                if (!use_buf) {
+                    {
+                        if (g.evol) {
+                            run(std::true_type{}, std::true_type{});
+                            return;
+                        }
+                    }
+                    run(std::false_type{}, std::true_type{});
                     return;
                 }
             }
-            run(std::false_type{});
+            if constexpr (DPL == 8 || DPL == 16) {
+                if (g.evol) {
+                    run(std::true_type{}, std::false_type{});
+                    return;
+                }
+            }
+            run(std::false_type{}, std::false_type{});
             return;
         }
     }
@@ -2417,10 +2469,10 @@ static hipError_t launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells
     // packed u16 recurrence: the plain int16 regime with P1, P2 <= 32768 (SGM_OCV_PK=0 at build time: ints)
     const int use_pk = SGM_OCV_PK != 0 && !SAT && sizeof(VT) == 2 && g.P1 <= 32768 && g.P2 <= 32768;
     // the plain kernel writes deficit records only on its packed branch (8 or 16 values per lane,
-    // buffer offsets); ocv_evol_mode decided g.evol from the same conditions, and the WTA reads
+    // buffer offsets or 64-lane rebased descriptors); ocv_evol_mode decided g.evol from the same conditions, and the WTA reads
     // deficits whenever it is set: refuse a frame where the two disagree rather than hand the WTA
     // int16 L volumes it would read as deficits (flagged kernels ignore evol and write full volumes)
-    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_buf && use_pk))
+    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_pk && (use_buf || (LPL == 64 && DPL == 16))))
         return hipErrorInvalidValue;
     if (total > 0)
         hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
@@ -2481,8 +2533,9 @@ static int ocv_paths_dpl(const Geom& g, int dirmask)
 }
 
 // Deficits (Geom::evol, load_e) for the plain kernels of a frame: P2 <= 511 (e in 9 bits), the
-// packed paths step (P1 <= 32768) with buffer offsets, 8 or 16 values per path lane (whole groups
-// of 8 per lane), D <= 512 (the row WTA k_ocv_wta16 or the fused vertical WTA read them). Returns
+// packed paths step (P1 <= 32768) with buffer offsets or 64-lane rebased descriptors, 8 or 16
+// values per path lane (whole groups of 8 per lane), D <= 512 (the row WTA k_ocv_wta16 or the
+// fused vertical WTA read them) or D <= 1024 under the fused vertical WTA. Returns
 // the layout (1 records, 2 planes for D % 128 == 0) or 0; SGM_OCV_EVOL=0 (environment or build
 // macro) keeps int16 L volumes, =1 / =2 forces a layout.
 #ifndef SGM_OCV_EVOL
@@ -2493,10 +2546,15 @@ int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
     if (SGM_OCV_EVOL == 0 || SGM_OCV_PK == 0) return 0;
     const char* e = std::getenv("SGM_OCV_EVOL");       // 0 off, 1 / 2 force a layout
     if (e && std::atoi(e) == 0) return 0;
-    if (g.wide == 1 || g.P2 > 511 || g.P1 > 32768 || g.D > 512 || g.width1 <= 0) return 0;
-    if ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF")) return 0;
-    const int dpl = ocv_paths_dpl(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
+    if (g.wide == 1 || g.P2 > 511 || g.P1 > 32768 || g.D > 1024 || g.width1 <= 0) return 0;
+    const int pmask = skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask;
+    const int dpl = ocv_paths_dpl(g, pmask);
     if (dpl != 8 && dpl != 16) return 0;
+    // 32-bit buffer offsets, or 64-lane lines of 16 values (rebased per step, any volume size)
+    const bool reb = ocv_lanes_per_line(g, pmask) == 64 && dpl == 16;
+    if (!reb && ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF"))) return 0;
+    // D > 512: only the fused vertical WTA reads deficits (the row WTA k_ocv_wta64 reads int16 L)
+    if (g.D > 512 && skipdir < 0) return 0;
     // the fused vertical WTA reads them from 8 values per lane (D > 256): with 2 or 4 the byte and
     // bit loads per direction cost more than they save (1080p D=128 MODE_HH 2.48 -> 2.95 ms)
     if (skipdir >= 0 && g.D <= 256) return 0;

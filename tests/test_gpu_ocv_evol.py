@@ -79,3 +79,46 @@ def test_evol_1080p_both_layouts(engine, synth, pkg, monkeypatch, mode):
         outs[evol] = engine.match(left, right)
     assert np.array_equal(outs["1"], outs["0"]), f"records: {(outs['1'] != outs['0']).sum()} pixels differ"
     assert np.array_equal(outs["2"], outs["0"]), f"planes: {(outs['2'] != outs['0']).sum()} pixels differ"
+
+
+# 64-lane lines of 16 values (512 < D <= 1024). With SGM_OCV_NO_BUF=1 the packed step rebases its
+# buffer descriptors on each step's cell — the form every frame whose volumes pass 4 GB takes (the
+# processing launch's D = 752 at 2448 x 2048: 5.2 GB) — and, under the fused vertical WTA, stores
+# deficit records (vwta 0: the row WTA k_ocv_wta64 reads int16 L, so no deficits there).
+REB_GEOMS = [(26, 900, 0, 752, 21), (22, 800, 7, 640, 9), (20, 1150, -3, 1024, 5), (24, 700, 0, 528, 15)]
+
+
+@pytest.mark.parametrize("nobuf", ["0", "1"], ids=["offsets", "rebased"])
+@pytest.mark.parametrize("evol", ["default", "0"], ids=["evol", "evol-off"])
+@pytest.mark.parametrize("vwta", ["0", "1"], ids=["wta64", "vwta"])
+@pytest.mark.parametrize("mode", [0, 1], ids=["SGBM", "HH"])
+@pytest.mark.parametrize("geom", REB_GEOMS, ids=[f"{g[0]}x{g[1]}-m{g[2]}-D{g[3]}-b{g[4]}" for g in REB_GEOMS])
+def test_wide_disparity_rebased_paths(engine, oracle, synth, pkg, monkeypatch, geom, mode, vwta, evol, nobuf):
+    h, w, minD, D, block = geom
+    if evol != "default":
+        monkeypatch.setenv("SGM_OCV_EVOL", evol)
+    monkeypatch.setenv("SGM_OCV_VWTA", vwta)
+    monkeypatch.setenv("SGM_OCV_NO_BUF", nobuf)
+    left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h * w + D + mode)
+    p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, uniqueness_ratio=2,
+                           speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.parametrize("uniq", [0, 100])
+@pytest.mark.parametrize("mode", [0, 1], ids=["SGBM", "HH"])
+def test_wide_disparity_rebased_uniqueness_edges(engine, oracle, synth, pkg, monkeypatch, mode, uniq):
+    """uniqueness 100 routes the fused vertical WTA to its int form (k_ocv_vwta) over the same
+    deficit records; 0 keeps the packed one."""
+    monkeypatch.setenv("SGM_OCV_VWTA", "1")
+    monkeypatch.setenv("SGM_OCV_NO_BUF", "1")
+    left, right, _ = synth.stereo_pair(24, 880, 0, 752, seed=752 + mode + uniq)
+    p = pkg.default_params(mode, min_disparity=0, num_disparities=752, block_size=21, uniqueness_ratio=uniq,
+                           speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
