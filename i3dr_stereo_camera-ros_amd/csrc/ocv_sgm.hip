@@ -553,6 +553,9 @@ template <int R, int DPC, int I, int TRK>
                                  // boxes up to this size (1080p block 5: 0.221 -> 0.217 ms; the shipped
                                  // block 21: 2.00 -> 2.05 ms, so not there; profiles/r05_ocv_pk_cost_ab.jsonl)
 #endif
+#ifndef SGM_FUSE_DPC16_PART
+#define SGM_FUSE_DPC16_PART 1    // 16 pairs per block row (a partial last chunk) for D % 32 == 16, D >= 256
+#endif
 #ifndef SGM_FUSE_WPE
 #define SGM_FUSE_WPE -1          // waves per SIMD asked of the compiler (4: <= 128 VGPRs); -1: 4 for R > 9
 #endif
@@ -662,6 +665,9 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     const bool edge = klo > 0 || khi < NX - 1;               // uniform: strips at the frame's sides
     const int bp = t % DPC, bseg = t / DPC;
     const int xa = bseg * L, xb = min(xa + L, nout);
+    // the last chunk of a frame whose D is not a multiple of DC holds pairs past D: computed
+    // (their right entries clamp inside the row) but never stored nor flagged
+    const bool pok = d0 + 2 * bp < gD;
     u16x2_t bmax = {0, 0};                                   // flag: the largest box sum seen
     const bool col0 = (gcompat & SGM_OCV_COL0_LEGACY) && x0 == 0;
     const u16x2_t p2v = {(unsigned short)gP2, (unsigned short)gP2};
@@ -791,7 +797,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
 #pragma unroll
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
-                    const bool ok = j < nj;
+                    const bool ok = j < nj && pok;
                     if constexpr (TRK != 0) {
                         const u16x2_t cand = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
                         bmax = (ok && !(j == 0 && skip0)) ? cand : bmax;
@@ -802,7 +808,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
 #pragma unroll
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
-                    if (xa + j < xb) {
+                    if (xa + j < xb && pok) {
                         if constexpr (TRK != 0)
                             if (!(col0 && xa + j == 0 && y > 0))
                                 bmax = __builtin_elementwise_max(bmax, TRK == 1 ? sum : sum - p2v);
@@ -821,7 +827,7 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 for (int j = 0; j < L; j++) {
                     if (j > 0) sum += w[j + R - 1] - w[j - 1];
                     const uint32_t c = fullDP ? gP2 * 0x10001u : as_u(sum);
-                    if (xa + j < xb)
+                    if (xa + j < xb && pok)
                         for (int yy = y + 1; yy < gH; yy++) o[(size_t)(yy - y) * rowC] = c;
                     o += gD / 2;
                 }
@@ -2256,10 +2262,13 @@ static int dpl_for(int D) { return D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : D <
 static int fuse_dpc(const Geom& g)
 {
     const int R = 2 * g.SH2 + 1;
-    int dpc = (R <= 9 && g.D % 64 == 0) ? 32 : g.D % 32 == 0 ? 16 : 8;
+    // D % 32 == 16 from D = 256 on: 16 pairs with a half-empty last chunk (<= 6 % of the pixel-cost
+    // work wasted) beat 8 pairs, whose blocks stage the same BT rows for half the disparities (the
+    // processing launch's D = 752 block 21: profiles/r06_ocv_cost_dpc_ab.jsonl)
+    int dpc = (R <= 9 && g.D % 64 == 0) ? 32 : (g.D % 32 == 0 || (g.D >= 256 && SGM_FUSE_DPC16_PART)) ? 16 : 8;
     if (const char* e = std::getenv("SGM_FUSE_DPC")) {
         const int f = std::atoi(e);
-        if ((f == 32 && R <= 9 && g.D % 64 == 0) || (f == 16 && g.D % 32 == 0) || f == 8) dpc = f;
+        if ((f == 32 && R <= 9 && g.D % 64 == 0) || f == 16 || f == 8) dpc = f;
     }
     return dpc;
 }
@@ -2312,7 +2321,7 @@ static FuseGrid fuse_grid(const Geom& g)
     const int dpc = fuse_dpc(g);
     const int XB = fuse_xb(g);
     fg.strips = (g.width1 + XB - 1) / XB;
-    fg.chunks = g.D / (2 * dpc);
+    fg.chunks = (g.D + 2 * dpc - 1) / (2 * dpc);   // the last one partly past D when 2 * dpc does not divide D
     fg.ncomp = std::max(g.H - g.SH2 - 1, 0) + 1;             // rows 0 .. ylast are computed
     const long long tiles = (long long)fg.strips * fg.chunks;
     // bands: about four rounds of blocks over the chip's slots (two 512-thread blocks per CU, every

@@ -37,7 +37,7 @@ GEOMS = [
     (17, 70, 2, 32, 3, 1, 0),
     (40, 200, 9, 64, 15, 31, 1),
     (30, 300, 0, 128, 11, 20, 7),
-    (130, 333, 5, 48, 9, 31, 0),        # D % 32 = 16: 8-pair blocks only
+    (130, 333, 5, 48, 9, 31, 0),        # D % 32 = 16: 16-pair blocks have a half-empty last chunk
     (70, 400, -8, 80, 21, 7, 7),        # block 21 with D % 32 = 16
     (150, 500, 0, 96, 1, 31, 1),        # block 1
     (64, 150, 10, 128, 5, 31, 7),       # width1 = 12: one narrow strip, both frame edges in it
@@ -45,6 +45,8 @@ GEOMS = [
     (90, 460, 3, 192, 17, 15, 1),
     (33, 900, 147, 480, 21, 7, 7),      # the shipped geometry's D, minD and box
     (26, 1200, 0, 256, 19, 11, 0),      # width1 > 7 strips
+    (24, 1000, 0, 752, 21, 7, 7),       # the processing launch's D = 752: 16-pair blocks, partial last chunk
+    (40, 620, 3, 272, 5, 31, 0),        # D % 32 = 16 above 256 (16 pairs by default)
 ]
 
 
