@@ -114,7 +114,7 @@ def test_census_and_wta_kernels_have_no_waterfall_loops(asm):
 
 # Instantiations allowed to use scratch, with the reason: 32 values per path lane are D > 1024, which
 # no configuration of the reference reaches (its widest search is D = 752); the shipped block-21 cost
-# kernel's 12 B are a spill of loop-invariant values outside its row loop.
+# kernel keeps ring slot 0's two words in 12 B of scratch (2 loads + 2 stores every 21 rows).
 SCRATCH_ALLOWED = ("_ZN3sgm10k_ocv_vwtaILi32E", "_ZN3sgm13k_ocv_vwta_pkILi32E", "_ZN3sgm16k_ocv_cost_fusedILi21ELi16ELi4E")
 
 
