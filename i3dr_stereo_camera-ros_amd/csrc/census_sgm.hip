@@ -162,13 +162,12 @@ __device__ __forceinline__ void wload(const uint8_t* src, uint32_t (&wd)[(DPL + 
     }
 }
 
-// the same from a raw buffer (base wave-uniform, byte offset off per lane); AUX: the cache
-// policy (default nt: streamed once; 16 = sc1, agent-coherent: the gated single frame's WTA)
-template <int DPL, int AUX = -1>
+// the same from a raw buffer (base wave-uniform, byte offset off per lane)
+template <int DPL>
 __device__ __forceinline__ void wload_buf(const uint8_t* base, uint32_t off, uint32_t (&wd)[(DPL + 3) / 4])
 {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
-    constexpr int aux = AUX >= 0 ? AUX : SGM_NT_LOAD ? 2 : 0;   // 2: nt (streamed once)
+    constexpr int aux = SGM_NT_LOAD ? 2 : 0;           // 2: nt (streamed once)
     if constexpr (DPL == 2) { wd[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, aux); }
     else if constexpr (DPL == 4) { wd[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, aux); }
     else if constexpr (DPL == 8) {
@@ -549,25 +548,6 @@ __device__ __forceinline__ void p16_seed(const uint8_t* src, const uint32_t (&im
     p16_relative<DPL, LPL>(Labs, Lr);
 }
 
-#if SGM_GATED_BUILD
-// Band-gated single frame (experiment builds; k_census_single16): the path blocks
-// count every finished band of kBandRows rows into cnt[band] with an agent-scope RELEASE (the
-// XCD's L2 written back: buffer_wbl2), the volume stores themselves the production nt stores; the
-// frame's WTA rows, dispatched after every path block of the same launch, poll their band's count
-// and then load the volumes with sc1 (agent-coherent) loads. Round 3 built the same hand-off with
-// sc1 write-through stores of every volume byte (C2 3.53 ms against 0.99 for the two launches).
-struct Bands {
-    int* cnt;                 // [n_bands] signals, zeroed before the launch
-    const int* expect;        // [n_bands]
-    const uint16_t* order;    // [H] the WTA rows in dispatch order (middle bands first)
-};
-constexpr int kBandRows = 16;
-__device__ __forceinline__ void band_release(int* c)
-{
-    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-#endif
-
 // The last sweep fused with the WTA (census_fused16 "up+WTA" blocks): the upward vertical
 // sweep (dir 1) of a frame whose other seven volumes are complete; at each step every line
 // holds L_1(x, y, .) in the WTA's 16-lanes-per-pixel layout, adds the seven stored costs of
@@ -592,11 +572,10 @@ __host__ __device__ constexpr size_t upwta_lds_bytes() { return (size_t)8 * 2 * 
 
 // NL lines of direction dir starting at base column xb (DPL disparities per lane, LPL
 // lanes per line; lds: 2 * RowSeg<DPL, LPL>::BUF codes).
-template <int DPL, bool EXACT, int LPL, bool FUSE = false, bool PRIO = false, bool SIG = false>
+template <int DPL, bool EXACT, int LPL, bool FUSE = false, bool PRIO = false>
 __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const uint64_t* __restrict__ cR,
                                          uint8_t* __restrict__ V, uint8_t* __restrict__ trash, const Geom& g, int dir,
-                                         int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{},
-                                         int* sigc = nullptr)
+                                         int xb, const PathLaunch16& pl, uint64_t* lds, const UpWta& uw = UpWta{})
 {
     static_assert(!FUSE || LPL == 16, "up+WTA blocks use 16 lanes per line (the WTA layout)");
     using RS = RowSeg<DPL, LPL>;
@@ -728,29 +707,11 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
     };
     // step s reads buf[s & 1] (holding segment s), then segment s + 1 (register set
     // (s + 1) % 4) goes to buf[(s + 1) & 1] and set s % 4 is reloaded with segment s + 4
-#if SGM_GATED_BUILD
-    // SIG: the band of each step in this block's sweep order (rows go up for ry < 0); after the
-    // step that ends a band (or the block's last step) every wave retires its stores, the
-    // workgroup meets, and one thread releases the band's count at agent scope
-    const int sig_dir = ry > 0 ? 1 : -1;
-    auto band_of = [&](int st) { return (ry > 0 ? st : g.H - 1 - st) / kBandRows; };
-#endif
     auto body = [&](int s, const uint64_t* bcur, uint64_t* bnext, uint64_t (&Rnext)[RS::NLOAD],
                     uint64_t (&Rfree)[RS::NLOAD]) {
         seg_load<DPL, LPL>(Rfree, sa, g, rx, ry, xb, min(s + 4, s1 - 1));
         step(s, bcur);
         seg_store<DPL, LPL>(bnext, Rnext, tid);
-#if SGM_GATED_BUILD
-        if constexpr (SIG) {
-            const bool last = s == s1 - 1 || (s < s1 - 1 && band_of(s + 1) != band_of(s));   // uniform
-            if (s < s1 && last) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) band_release(sigc + band_of(s));
-            }
-        }
-        (void)sig_dir;
-#endif
         __syncthreads();
     };
     for (int s = s0; s < s1; s += 4) {
@@ -767,10 +728,9 @@ __device__ __forceinline__ void p16_rows(const uint64_t* __restrict__ cL, const 
 template <int DPL>
 __host__ __device__ constexpr int rows_lds_codes() { return 2 * RowSeg<RowsCfg<DPL>::DPL, RowsCfg<DPL>::LPL>::BUF; }
 
-template <int DPL, bool EXACT, bool PRIO = false, bool SIG = false>
+template <int DPL, bool EXACT, bool PRIO = false>
 __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_bytes, size_t trash_off,
-                                              const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds,
-                                              int* sigc = nullptr)
+                                              const Geom& g, const PathLaunch16& pl, uint32_t it, uint64_t* lds)
 {
     using RC = RowsCfg<DPL>;
     using HC = LineCfg<DPL>;
@@ -785,17 +745,7 @@ __device__ __forceinline__ void paths_block16(const PathFrames& pf, size_t vol_b
     const int y0 = lb * HC::HROWS + (64 / HC::LPL) * (threadIdx.x >> 6);
     if (dir == 6) p16_horiz<HC::DPL, EXACT, 1, PRIO, HC::LPL>(cL, cR, V, trash, g, y0);
     else if (dir == 7) p16_horiz<HC::DPL, EXACT, -1, PRIO, HC::LPL>(cL, cR, V, trash, g, y0);
-    else p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO, SIG>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl,
-                                                             lds, UpWta{}, sigc);
-#if SGM_GATED_BUILD
-    if constexpr (SIG) {
-        if (dir >= 6) {                    // the block's HROWS (= kBandRows) rows are band lb
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) band_release(sigc + lb);
-        }
-    }
-#endif
+    else p16_rows<RC::DPL, EXACT, RC::LPL, false, PRIO>(cL, cR, V, trash, g, dir, pl.xb_lo[dir] + lb * RC::NL, pl, lds);
 }
 
 // SGM_TRACE debug timeline: one 4 x u64 record per wave {tag | blockIdx << 32, XCC_ID << 32 |
@@ -928,7 +878,7 @@ __device__ __forceinline__ void wta_emask(int p, const Geom& g, uint32_t (&emask
 }
 
 // One image row y (one workgroup). lds: wta_lds_bytes<DPL>(W) bytes.
-template <int DPL, bool EXACT, typename OutT = int16_t, int AUX = -1>
+template <int DPL, bool EXACT, typename OutT = int16_t>
 __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size_t vol_bytes, const Geom& g,
                                           OutT* __restrict__ out, size_t out_stride, int y, uint32_t* lds)
 {
@@ -961,7 +911,7 @@ __device__ __forceinline__ void wta_row16(const uint8_t* __restrict__ vols, size
 #pragma unroll
         for (int vv = 0; vv < 8; vv++) {
             if ((SGM_EXP & 4) && vv == 1) { for (int j = 0; j < NWD; j++) v[vv][j] = 0; continue; }
-            wload_buf<DPL, AUX>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
+            wload_buf<DPL>(rowq + (size_t)vv * vol_bytes, loff, v[vv]);
         }
     };
     // S in u16 pairs (wta_pix16). The next pixel group's loads are summed at the end of an
@@ -1139,38 +1089,6 @@ void k_census_fused16(PathFrames pf, WtaFrames wf, CensusFrames cf, size_t vol_b
         trace_record(trace, (kind == 0 ? items[idx] : 0u) | ((uint64_t)kind << 62), t0);
 }
 
-#if SGM_GATED_BUILD
-// One frame in one launch with its WTA overlapped: blocks [0, n_items) are the frame's path
-// work list (SIG: band releases), blocks [n_items, n_items + H) its WTA rows in bd.order, each
-// waiting for its band. Every path block has a lower block id than every WTA block, so all path
-// blocks are dispatched before the first WTA row can hold a slot: a waiting row never keeps a
-// path block from running. The poll is bounded (~4 s); a frame that hit the bound would be
-// wrong, not hung. D <= 256 only (16-row horizontal blocks = one band).
-template <int DPL, bool EXACT>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(SGM_WPE)))
-void k_census_single16(PathFrames pf, WtaFrames wf, size_t vol_bytes, size_t trash_off, Geom g, PathLaunch16 pl,
-                       const uint32_t* __restrict__ items, int n_items, size_t out_stride, Bands bd)
-{
-    extern __shared__ uint64_t lds_dyn64[];
-    const int b = blockIdx.x;
-    if (b < n_items) {
-        paths_block16<DPL, EXACT, true, true>(pf, vol_bytes, trash_off, g, pl, items[b], lds_dyn64, bd.cnt);
-        return;
-    }
-    const int y = bd.order[b - n_items];
-    if (threadIdx.x == 0) {
-        int* c = bd.cnt + y / kBandRows;
-        const int want = bd.expect[y / kBandRows];
-        for (int it = 0; it < (1 << 22); it++) {
-            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    __syncthreads();
-    wta_row16<DPL, EXACT, int16_t, 16>(wf.vols[0], vol_bytes, g, wf.out[0], out_stride, y, (uint32_t*)lds_dyn64);
-}
-#endif
-
 // disp2 + LR check + store of one row from the up+WTA results: block b = row b % H of frame
 // b / H of wf (wf.res in, wf.out written)
 __global__ __launch_bounds__(kWG) void k_census_rowfin(WtaFrames wf, Geom g, size_t out_stride)
@@ -1276,72 +1194,6 @@ int census_path_items(const Geom& g, unsigned dir_mask, int n_slots, int group, 
     }
     return n;
 }
-
-#if SGM_GATED_BUILD
-int census_band_plan(const Geom& g, int* expect, uint16_t* order)
-{
-    const int nb = (g.H + kBandRows - 1) / kBandRows;
-    if (!expect) return nb;
-    for (int b = 0; b < nb; b++) expect[b] = 2;                 // dirs 6 and 7: one block per band
-    const PathLaunch16 pl = make_path_launch16(g);
-    const int NL = rows_lines(g.D);
-    for (int dir = 0; dir < 6; dir++) {
-        const int rx = dir_rx(dir), ry = dir_ry(dir);
-        const int hi = g.maxX1 + (rx < 0 ? g.H - 1 : 0);
-        const int nblk = (hi - pl.xb_lo[dir] + NL - 1) / NL;
-        for (int k = 0; k < nblk; k++) {
-            const int xb = pl.xb_lo[dir] + k * NL;
-            int s0, s1;      // p16_rows' step range
-            if (rx == 0) { s0 = 0; s1 = g.H; }
-            else if (rx > 0) { s0 = std::max(0, g.minX1 - xb - (NL - 1)); s1 = std::min(g.H, g.maxX1 - xb); }
-            else { s0 = std::max(0, xb - g.maxX1 + 1); s1 = std::min(g.H, xb + NL - g.minX1); }
-            if (s0 >= s1) continue;
-            const int ylo = ry > 0 ? s0 : g.H - s1, yhi = ry > 0 ? s1 - 1 : g.H - 1 - s0;
-            for (int b = ylo / kBandRows; b <= yhi / kBandRows; b++) expect[b]++;
-        }
-    }
-    int n = 0;
-    const int mid = (nb - 1) / 2;
-    for (int d = 0; d <= nb; d++)
-        for (int side = 0; side < 2; side++) {
-            const int b = side == 0 ? mid - d : mid + 1 + d;
-            if (b < 0 || b >= nb) continue;
-            for (int y = b * kBandRows; y < std::min(g.H, (b + 1) * kBandRows); y++) order[n++] = (uint16_t)y;
-        }
-    return nb;
-}
-
-template <int DPL>
-static void launch_single_dpl(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, size_t trash_off,
-                              const Geom& g, const PathLaunch16& pl, const uint32_t* items, int n_items,
-                              size_t out_stride, const Bands& bd, hipStream_t st)
-{
-    const size_t lds = std::max(wta_lds_bytes<DPL>(g.W), sizeof(uint64_t) * rows_lds_codes<DPL>());
-    dim3 grid(n_items + g.H), block(kWG);
-    if (g.D == 16 * DPL)
-        hipLaunchKernelGGL((k_census_single16<DPL, true>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride, bd);
-    else
-        hipLaunchKernelGGL((k_census_single16<DPL, false>), grid, block, lds, st, pf, wf, vol_bytes, trash_off, g, pl,
-                           items, n_items, out_stride, bd);
-}
-
-// the band-gated single frame (bd.cnt zeroed by the caller); D <= 256
-hipError_t launch_census_single(const PathFrames& pf, const WtaFrames& wf, size_t vol_bytes, const Geom& g,
-                                const uint32_t* items, int n_items, size_t out_stride, const Bands& bd, hipStream_t st)
-{
-    const PathLaunch16 pl = make_path_launch16(g);
-    const size_t trash_off = (size_t)g.H * g.width1 * g.D;
-    switch (dpl16_for(g.D)) {
-    case 2: launch_single_dpl<2>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 4: launch_single_dpl<4>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 8: launch_single_dpl<8>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    case 16: launch_single_dpl<16>(pf, wf, vol_bytes, trash_off, g, pl, items, n_items, out_stride, bd, st); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-#endif
 
 // SGM_TRACE=<file>: debug timeline of path / fused launches (one record per wave), written
 // after a synchronise by trace_dump. Never set in production runs.

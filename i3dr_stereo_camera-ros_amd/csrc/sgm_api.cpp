@@ -39,12 +39,6 @@ hipError_t launch_census_tiles(const CensusFrames&, int, int, hipStream_t);
 hipError_t launch_census_fused(const PathFrames&, const WtaFrames&, const CensusFrames&, size_t, const Geom&,
                                const uint32_t*, int, size_t, bool, hipStream_t);
 hipError_t launch_census_rowfin(const WtaFrames&, const Geom&, size_t, hipStream_t);
-#if SGM_GATED_BUILD
-struct Bands { int* cnt; const int* expect; const uint16_t* order; };
-int census_band_plan(const Geom&, int*, uint16_t*);
-hipError_t launch_census_single(const PathFrames&, const WtaFrames&, size_t, const Geom&, const uint32_t*, int, size_t,
-                                const Bands&, hipStream_t);
-#endif
 hipError_t launch_median3(const int16_t*, size_t, int16_t*, size_t, int, int, hipStream_t);
 hipError_t launch_speckle(const int16_t*, size_t, int16_t*, size_t, int, int, int, int, int, int*, int*, hipStream_t);
 hipError_t launch_fill16(int16_t*, size_t, int, int, int, hipStream_t);
@@ -550,37 +544,10 @@ int run_pipeline(sgm_handle* h, const Layout& l, const Geom& g, const uint8_t* d
         sgm::WtaFrames wf{};
         wf.vols[0] = vols; wf.out[0] = dst; wf.n = 1;
         if (outf) { wf.outf[0] = outf; wf.outf_stride = outf_stride; }
-#if SGM_GATED_BUILD
-        // experiment builds: the band-gated single frame (SGM_GATED=1; D <= 256, int16 output)
-        if (std::getenv("SGM_GATED") && std::atoi(std::getenv("SGM_GATED")) != 0 && g.D <= 256 && !outf) {
-            static void* dev = nullptr;        // cnt | expect | order (A/B tool only: one handle)
-            static std::string key;
-            const int nb = sgm::census_band_plan(g, nullptr, nullptr);
-            const size_t bytes = (size_t)8 * nb + (size_t)2 * g.H;
-            char k2[96];
-            snprintf(k2, sizeof k2, "%d %d %d %d", g.W, g.H, g.D, g.minD);
-            if (key != k2) {
-                if (dev) (void)hipFree(dev);
-                HIP_TRY(hipMalloc(&dev, bytes), "hipMalloc bands");
-                std::vector<char> host(bytes);
-                sgm::census_band_plan(g, (int*)(host.data() + (size_t)4 * nb), (uint16_t*)(host.data() + (size_t)8 * nb));
-                HIP_TRY(hipMemcpy(dev, host.data(), bytes, hipMemcpyHostToDevice), "H2D bands");
-                key = k2;
-            }
-            sgm::Bands bd{(int*)dev, (const int*)((char*)dev + (size_t)4 * nb), (const uint16_t*)((char*)dev + (size_t)8 * nb)};
-            HIP_TRY(hipMemsetAsync(bd.cnt, 0, sizeof(int) * nb, st), "hipMemsetAsync");
-            rec.begin("paths8+wta_lr", 16 * cells + 2 * WH);
-            HIP_TRY(sgm::launch_census_single(pf, wf, l.vol_bytes, g, items, n_items, dst_stride, bd, st), "single");
-            goto census_done;
-        }
-#endif
         rec.begin("paths8", 8 * cells);
         HIP_TRY(sgm::launch_census_paths(pf, l.vol_bytes, g, items, n_items, st), "paths");
         rec.begin("wta_lr", 8 * cells + 2 * WH);
         HIP_TRY(sgm::launch_census_wta(wf, l.vol_bytes, g, dst_stride, st), "wta");
-#if SGM_GATED_BUILD
-    census_done:;
-#endif
     } else {
         const int fullDP = p.mode == SGM_MODE_OCV_HH8;
         const int mask = fullDP ? 0xFF : 0xCD;   // SGBM5: dirs 0,2,3,6,7
