@@ -2728,8 +2728,13 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
     // steps in flight: a column is one latency-bound chain (width1 waves, ~2 per SIMD), and the
     // packed operands are half the registers of k_ocv_vwta's ints. 16 values per lane (D > 512):
     // 8 steps of MODE_HH operands are 512 VGPRs (904 B/lane of scratch: the D=752 processing
-    // config's kernel 21.3 ms), 2 or 4 steps fit (7.85 ms; profiles/r06_ocv_d752_vwta_ab.jsonl)
-    constexpr int PF = SGM_OCV_VWTA_PK_PF > 0 ? SGM_OCV_VWTA_PK_PF : DPL >= 32 ? 1 : DPL >= 16 ? 2 : 8;
+    // config's kernel 21.3 ms), 2 or 4 steps fit (7.85 ms; profiles/r06_ocv_d752_vwta_ab.jsonl); with
+    // deficit records MODE_HH keeps 2 (5.67 ms against 7.4-7.6 at 3-4) and MODE_SGBM takes 4 (4.36-4.39
+    // against 4.52-4.54 at 2; profiles/r06_ocv_d752_vwta_pf_ab.jsonl)
+    constexpr int PF = SGM_OCV_VWTA_PK_PF > 0 ? SGM_OCV_VWTA_PK_PF
+                       : DPL >= 32                ? 1
+                       : DPL >= 16                ? (NDIR == 5 ? 4 : 2)
+                                                  : 8;
     const int p = threadIdx.x;
     const int x1 = blockIdx.x;
     const bool lanetie = NDIR == 5 && (g.compat & SGM_OCV_LANE_TIE);
