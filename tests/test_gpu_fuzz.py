@@ -80,7 +80,8 @@ def test_fuzz_match(engine, oracle, synth, pkg, seed):
     left, right = _images(rng, synth, h, w, kw["min_disparity"], kw["num_disparities"], kind, seed)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
-    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
+    env = {k: os.environ.get(k) for k in ("SGM_OCV_NO_BUF", "SGM_OCV_VWTA")}
+    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind} {env}: {(got != ref).sum()} pixels differ"
 
 
 def _ocv_fusable(h, w, kw):
@@ -324,10 +325,17 @@ def test_fuzz_host_batch_and_overlap_tiles(engine, oracle, synth, pkg, seed):
 
 
 @pytest.mark.parametrize("seed", range(max(N_CASES // 4, 8)))
-def test_fuzz_ocv_large_disparity(engine, oracle, synth, pkg, seed):
+def test_fuzz_ocv_large_disparity(engine, oracle, synth, pkg, monkeypatch, seed):
     """OpenCV modes with D > 512 (64-lane path lines, chunked one-pixel-per-wave WTA): random
-    windows up to the cfg's 2048, blocks, penalties, uniqueness and post filters."""
+    windows up to the cfg's 2048, blocks, penalties, uniqueness and post filters; half the cases
+    with the step-rebased path descriptors forced (SGM_OCV_NO_BUF=1: the form of volumes past
+    4 GB) and half with the fused vertical WTA forced (its deficit records for D <= 1024)."""
     rng = np.random.default_rng(50_000 + seed)
+    sub = np.random.default_rng(70_000 + seed)          # the switches, apart from the case draws
+    if sub.random() < 0.5:
+        monkeypatch.setenv("SGM_OCV_NO_BUF", "1")
+    if sub.random() < 0.5:
+        monkeypatch.setenv("SGM_OCV_VWTA", "1")
     mode = [pkg.MODE_OCV_SGBM5, pkg.MODE_OCV_HH8][seed % 2]
     D = int(rng.choice([528, 640, 768, 1024, 1296, 1536, 2048]))
     minD = int(rng.integers(-12, 13))
@@ -346,4 +354,5 @@ def test_fuzz_ocv_large_disparity(engine, oracle, synth, pkg, seed):
     left, right = _images(rng, synth, h, w, minD, min(D, 256), kind, seed)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
-    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind}: {(got != ref).sum()} pixels differ"
+    env = {k: os.environ.get(k) for k in ("SGM_OCV_NO_BUF", "SGM_OCV_VWTA")}
+    assert np.array_equal(got, ref), f"mode {mode} {h}x{w} {kw} {kind} {env}: {(got != ref).sum()} pixels differ"
