@@ -508,6 +508,18 @@ __host__ __device__ inline int fuse_xb(const Geom& g) { return kFuseNX - 2 * g.S
 // rows per barrier: RB rows of pixel costs, boxes and staging between two barriers, the box RB
 // rows behind the pixel costs and the staging RB rows ahead, over 2 * RB LDS buffers each
 __host__ __device__ constexpr int fuse_rb(int R) { return (R > 9 && SGM_FUSE_RB2 != 0) ? 2 : 1; }
+#ifndef SGM_FUSE_RING8
+#define SGM_FUSE_RING8 1         // the pixel-cost ring as bytes (half the registers)
+#endif
+#ifndef SGM_FUSE_RING0_LDS
+#define SGM_FUSE_RING0_LDS 1     // boxes wider than 9: ring slot 0 kept in LDS (hipcc had spilled it to scratch)
+#endif
+// words of LDS that hold ring slot 0 (R > 9): one per ring register of every thread
+__host__ __device__ constexpr int fuse_ring0_words(int r, int dpc)
+{
+    // RQ ring registers per thread: I = dpc / 4 disparity pairs, two per register as bytes (SGM_FUSE_RING8)
+    return (SGM_FUSE_RING0_LDS != 0 && r > 9) ? (SGM_FUSE_RING8 != 0 ? dpc / 8 : dpc / 4) * kFuseThreads : 0;
+}
 struct FuseGeo {
     int DC, M, MH;
     __host__ __device__ FuseGeo(int dpc) {
@@ -520,8 +532,9 @@ struct FuseGeo {
         if (dpc == 32) MH += ((5 - MH % 8) + 8) % 8;
     }
     __host__ __device__ int stage_words() const { return 6 * kFuseNX + 14 * MH; }
-    __host__ __device__ size_t lds_bytes(int dpc, int rb) const {
-        return (size_t)4 * 2 * rb * (stage_words() + kFuseNX * dpc);
+    // + ring slot 0 in LDS for boxes wider than 9 (fuse_ring0_words)
+    __host__ __device__ size_t lds_bytes(int dpc, int rb, int r = 0) const {
+        return (size_t)4 * 2 * rb * (stage_words() + kFuseNX * dpc) + (size_t)4 * fuse_ring0_words(r, dpc);
     }
 };
 struct FuseGrid {
@@ -536,9 +549,6 @@ template <int R, int DPC, int I, int TRK>
 // plus <= 128 VGPRs asked for R > 9 (two blocks per CU at 36 B of spills) -> 2.86 ms; the box reads issued
 // before the pixel costs instead of after the V store: 3.73 ms at R = 21 (the window registers live across
 // the pixel-cost phase), no gain at R = 5
-#ifndef SGM_FUSE_RING8
-#define SGM_FUSE_RING8 1         // the pixel-cost ring as bytes (half the registers)
-#endif
 #ifndef SGM_FUSE_BOX_EARLY
 #define SGM_FUSE_BOX_EARLY 0     // the box reads issued before the pixel costs (else after the V store)
 #endif
@@ -652,6 +662,15 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
     for (int q = 0; q < RQ; q++)
 #pragma unroll
         for (int s2 = 0; s2 < R; s2++) ring[q][s2] = 0;
+    // ring slot 0 in LDS for wide boxes (each thread its own words: no barrier; read and written
+    // once every R rows): at <= 128 VGPRs hipcc spilled that slot to scratch, whose reload put a
+    // vmcnt(0) wait (the row's C' stores and BT loads) into every R-th row
+    constexpr bool kRing0Lds = fuse_ring0_words(R, DPC) > 0;
+    uint32_t* ring0 = lds_fuse + NBUF * fz.stage_words() + NBUF * kFuseNX * DPC + t;
+    if constexpr (kRing0Lds) {
+#pragma unroll
+        for (int q = 0; q < RQ; q++) ring0[q * kFuseThreads] = 0;
+    }
     auto sat = [](u16x2_t a, u16x2_t b) { return __builtin_elementwise_sub_sat(a, b); };
     auto wd = [](const uint32_t* p, int o) { return __builtin_bit_cast(u16x2_t, p[o]); };
     // box: thread (segment, pair); NB box threads, L outputs per segment, the NL = L + R - 1
@@ -734,16 +753,19 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
                 if constexpr (kRing8) {
 #pragma unroll
                     for (int h = 0; h < RQ; h++) {
-                        const uint32_t o = ring[h][s2];
+                        const uint32_t o = (kRing0Lds && s2 == 0) ? ring0[h * kFuseThreads] : ring[h][s2];
                         vupd(2 * h, __builtin_amdgcn_perm(o, o, 0x0C010C00u));       // bytes 0, 1 -> u16 lanes
                         vupd(2 * h + 1, __builtin_amdgcn_perm(o, o, 0x0C030C02u));   // bytes 2, 3
-                        ring[h][s2] = __builtin_amdgcn_perm(P[2 * h + 1], P[2 * h], 0x06040200u);
+                        const uint32_t nw = __builtin_amdgcn_perm(P[2 * h + 1], P[2 * h], 0x06040200u);
+                        if (kRing0Lds && s2 == 0) ring0[h * kFuseThreads] = nw;
+                        else ring[h][s2] = nw;
                     }
                 } else {
 #pragma unroll
                     for (int q = 0; q < I; q++) {
-                        vupd(q, ring[q][s2]);
-                        ring[q][s2] = P[q];
+                        vupd(q, (kRing0Lds && s2 == 0) ? ring0[q * kFuseThreads] : ring[q][s2]);
+                        if (kRing0Lds && s2 == 0) ring0[q * kFuseThreads] = P[q];
+                        else ring[q][s2] = P[q];
                     }
                 }
             };
@@ -2291,17 +2313,24 @@ static void launch_cost_fused_rt(const uint32_t* bt, const Geom& g, int fullDP, 
     const int dpc = fuse_dpc(g);
     if constexpr (R <= 9) {
         if (dpc == 32) {
-            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8, TRK>), grid, block, FuseGeo(32).lds_bytes(32, fuse_rb(R)), st, bt, g,
+            hipLaunchKernelGGL((k_ocv_cost_fused<R, 32, 8, TRK>), grid, block, FuseGeo(32).lds_bytes(32, fuse_rb(R), R), st, bt, g,
                                fullDP, fg, C);
             return;
         }
     }
-    if (dpc == 16)
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4, TRK>), grid, block, FuseGeo(16).lds_bytes(16, fuse_rb(R)), st, bt, g, fullDP,
-                           fg, C);
-    else
-        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2, TRK>), grid, block, FuseGeo(8).lds_bytes(8, fuse_rb(R)), st, bt, g, fullDP,
-                           fg, C);
+    // blocks above 64 KB of LDS (R > 9: two rows per barrier plus ring slot 0) ask for it
+    auto allow = [](const void* k, size_t lds) {
+        if (lds > 65536) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    };
+    if (dpc == 16) {
+        const size_t lds = FuseGeo(16).lds_bytes(16, fuse_rb(R), R);
+        allow(reinterpret_cast<const void*>(&k_ocv_cost_fused<R, 16, 4, TRK>), lds);
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 16, 4, TRK>), grid, block, lds, st, bt, g, fullDP, fg, C);
+    } else {
+        const size_t lds = FuseGeo(8).lds_bytes(8, fuse_rb(R), R);
+        allow(reinterpret_cast<const void*>(&k_ocv_cost_fused<R, 8, 2, TRK>), lds);
+        hipLaunchKernelGGL((k_ocv_cost_fused<R, 8, 2, TRK>), grid, block, lds, st, bt, g, fullDP, fg, C);
+    }
 }
 
 template <int R>
@@ -2730,10 +2759,13 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
     // 8 steps of MODE_HH operands are 512 VGPRs (904 B/lane of scratch: the D=752 processing
     // config's kernel 21.3 ms), 2 or 4 steps fit (7.85 ms; profiles/r06_ocv_d752_vwta_ab.jsonl); with
     // deficit records MODE_HH keeps 2 (5.67 ms against 7.4-7.6 at 3-4) and MODE_SGBM takes 4 (4.36-4.39
-    // against 4.52-4.54 at 2; profiles/r06_ocv_d752_vwta_pf_ab.jsonl)
+    // against 4.52-4.54 at 2; profiles/r06_ocv_d752_vwta_pf_ab.jsonl). 8 values per lane: MODE_HH over
+    // deficit records 4 (the shipped D=480 frame's kernel 4.77 -> 3.68 ms), else 8 (MODE_SGBM 2.95
+    // against 3.04 at 4, 2.99 at 6; profiles/r06_ocv_cost_ring0_vwta_pf_ab.jsonl)
     constexpr int PF = SGM_OCV_VWTA_PK_PF > 0 ? SGM_OCV_VWTA_PK_PF
                        : DPL >= 32                ? 1
                        : DPL >= 16                ? (NDIR == 5 ? 4 : 2)
+                       : (NDIR == 8 && EV)        ? 4
                                                   : 8;
     const int p = threadIdx.x;
     const int x1 = blockIdx.x;

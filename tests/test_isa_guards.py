@@ -113,9 +113,9 @@ def test_census_and_wta_kernels_have_no_waterfall_loops(asm):
 
 
 # Instantiations allowed to use scratch, with the reason: 32 values per path lane are D > 1024, which
-# no configuration of the reference reaches (its widest search is D = 752); the shipped block-21 cost
-# kernel keeps ring slot 0's two words in 12 B of scratch (2 loads + 2 stores every 21 rows).
-SCRATCH_ALLOWED = ("_ZN3sgm10k_ocv_vwtaILi32E", "_ZN3sgm13k_ocv_vwta_pkILi32E", "_ZN3sgm16k_ocv_cost_fusedILi21ELi16ELi4E")
+# no configuration of the reference reaches (its widest search is D = 752). (The shipped block-21 cost
+# kernel had kept ring slot 0 in 12 B of scratch until round 6; that slot now lives in LDS.)
+SCRATCH_ALLOWED = ("_ZN3sgm10k_ocv_vwtaILi32E", "_ZN3sgm13k_ocv_vwta_pkILi32E")
 
 
 def test_no_scratch_spills(tmp_path):
@@ -123,4 +123,3 @@ def test_no_scratch_spills(tmp_path):
     assert len(sizes) > 200, f"expected the library's kernels, found {len(sizes)}"
     bad = {k: v for k, v in sizes.items() if v > 0 and not k.startswith(SCRATCH_ALLOWED)}
     assert not bad, f"kernels spilling to scratch: {bad}"
-    assert max(v for k, v in sizes.items() if k.startswith("_ZN3sgm16k_ocv_cost_fused")) <= 16
