@@ -1288,6 +1288,9 @@ __device__ __forceinline__ long long uni64(long long v)
 #ifndef SGM_OCV_PK_PF
 #define SGM_OCV_PK_PF 16   // packed path lines: cost rows in flight for up to 4 dwords per lane (4 for 8, 2 for 16)
 #endif
+#ifndef SGM_OCV_PK_PF8
+#define SGM_OCV_PK_PF8 8   // packed 64-lane path lines of 16 values: cost rows in flight
+#endif
 #ifndef SGM_OCV_PK
 #define SGM_OCV_PK 1       // the plain int16 path recurrence in packed u16 pairs (0: one int per value)
 #endif
@@ -1497,7 +1500,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             // (1080p D=128 MODE_SGBM paths, M = 4: 0.97 ms unpacked, packed 0.91 / 0.86 / 0.84 at 4 / 8 /
             // 16 rows; the shipped D=480 config, M = 8: 6.20 ms unpacked and at 4 rows, 6.79 at 8;
             // profiles/r05_ocv_pk_ab.jsonl)
-            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? 4 : 2;
+            // 16 values per lane on 64-lane lines (512 < D <= 1024, the rebased form): 8 rows
+            // (the D=752 config's paths 7.49 -> 7.27 ms MODE_SGBM, 13.29 -> 12.95 MODE_HH; 2 / 3 / 6:
+            // 7.48-7.51 / 7.44; profiles/r06_ocv_paths_pf8_ab.jsonl)
+            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? (LPL == 64 ? SGM_OCV_PK_PF8 : 4) : 2;
             // deficits (Geom::evol, 8 or 16 values per lane): the low bytes and the bits of d
             const EvLayout el = evol_layout(g);
             const long long pix0 = (long long)ybase * g.width1 + x0, pstep = (long long)ry * g.width1 + rx;
