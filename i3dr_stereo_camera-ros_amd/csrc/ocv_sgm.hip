@@ -1288,6 +1288,9 @@ __device__ __forceinline__ long long uni64(long long v)
 #ifndef SGM_OCV_PK_PF
 #define SGM_OCV_PK_PF 16   // packed path lines: cost rows in flight for up to 4 dwords per lane (4 for 8, 2 for 16)
 #endif
+#ifndef SGM_OCV_PK_PF16
+#define SGM_OCV_PK_PF16 12 // packed 16-lane path lines of <= 8 values: cost rows in flight
+#endif
 #ifndef SGM_OCV_PK_PF8
 #define SGM_OCV_PK_PF8 8   // packed 64-lane path lines of 16 values: cost rows in flight
 #endif
@@ -1503,7 +1506,12 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             // 16 values per lane on 64-lane lines (512 < D <= 1024, the rebased form): 8 rows
             // (the D=752 config's paths 7.49 -> 7.27 ms MODE_SGBM, 13.29 -> 12.95 MODE_HH; 2 / 3 / 6:
             // 7.48-7.51 / 7.44; profiles/r06_ocv_paths_pf8_ab.jsonl)
-            constexpr int PF = M <= 4 ? SGM_OCV_PK_PF : M <= 8 ? (LPL == 64 ? SGM_OCV_PK_PF8 : 4) : 2;
+            // <= 4 dwords per lane: 16 rows, 12 on 16-lane lines (1080p D=128 paths MODE_SGBM 0.812 ->
+            // 0.798 ms, MODE_HH 1.257 -> 1.203; 8 / 24: 0.803 / 0.816, 1.219 / 1.326; the shipped D=480
+            // 64-lane lines keep 16: 5.34 against 5.40 / 5.51 at 12 / 8, 5.31 at 24;
+            // profiles/r06_ocv_paths_pf_m4_ab.jsonl)
+            constexpr int PF = M <= 4 ? (LPL == 16 ? SGM_OCV_PK_PF16 : SGM_OCV_PK_PF)
+                             : M <= 8 ? (LPL == 64 ? SGM_OCV_PK_PF8 : 4) : 2;
             // deficits (Geom::evol, 8 or 16 values per lane): the low bytes and the bits of d
             const EvLayout el = evol_layout(g);
             const long long pix0 = (long long)ybase * g.width1 + x0, pstep = (long long)ry * g.width1 + rx;
