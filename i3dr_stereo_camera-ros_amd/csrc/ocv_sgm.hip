@@ -1395,7 +1395,9 @@ __device__ __forceinline__ void evol_store(__amdgpu_buffer_rsrc_t rs, uint32_t l
 // line - width1 + 1. The lines of a block have (nearly) equal lengths; each stores only
 // while its own steps last. Fewer, wider lines (LPL 32) shorten each step's instruction
 // chain: a line is a sequential walk, and its step latency bounds the kernel.
-template <int DPL, int LPL, typename VT, bool SAT>
+// REBK: the instantiation for 64-lane lines of 8 values whose volumes pass 4 GB (the step-rebased
+// packed form only; kept apart so its descriptors' SGPRs do not weigh on the buffer-offset kernel)
+template <int DPL, int LPL, typename VT, bool SAT, bool REBK = false>
 __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C, VT* __restrict__ vols,
                                                   size_t vol_elems, size_t trash_off, Geom g, int dirmask, int4 nblk0,
                                                   int4 nblk1, int use_buf, int use_pk, int ilv)
@@ -1482,11 +1484,12 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         // cell is wave-uniform) — any size, each step's descriptors rebased on the step's cell
         // (64-bit scalar arithmetic, lane offsets within the cell): the D > 512 frames (the
         // processing launch's D = 752 has 5.2 GB int16 volumes) keep the packed step and the
-        // deficit records. Only 16 values per lane (512 < D <= 1024) take it: in the 8-value
-        // instantiation the per-step descriptors of 16 rows in flight cost SGPRs the buffer-offset
-        // form of the same kernel (the shipped D=480 config) would pay for (105 -> 138 VGPRs), and
-        // 32 values (D > 1024) have a lane straddling D that would load past its rebased cell.
-        if (use_pk && (use_buf || (LPL == 64 && DPL == 16))) {
+        // deficit records. 16 values per lane (512 < D <= 1024) in this kernel; 8 values (256 < D <=
+        // 512 on frames past 4 GiB of volume, e.g. 12 MP) in their own instantiation (REBK), because
+        // the per-step descriptors of 16 rows in flight cost SGPRs that the buffer-offset form of the
+        // same kernel (the shipped D=480 config) would otherwise pay for (105 -> 138 VGPRs); 32 values
+        // (D > 1024) have a lane straddling D that would load past its rebased cell.
+        if (use_pk && (use_buf || (LPL == 64 && (DPL == 16 || REBK)))) {
             constexpr int M = DPL / 2;
             const size_t cells = (size_t)g.width1 * g.H * g.D;
             const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(uint32_t)(cells * 2), 0x00020000);
@@ -1577,7 +1580,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                     steps(i0);
                 }
             };
-            if constexpr (LPL == 64 && DPL == 16) {
+            if constexpr (LPL == 64 && (DPL == 16 || REBK)) {
                 if (!use_buf) {
                     {
                         if (g.evol) {
@@ -2524,10 +2527,17 @@ static hipError_t launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells
     // buffer offsets or 64-lane rebased descriptors); ocv_evol_mode decided g.evol from the same conditions, and the WTA reads
     // deficits whenever it is set: refuse a frame where the two disagree rather than hand the WTA
     // int16 L volumes it would read as deficits (flagged kernels ignore evol and write full volumes)
-    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_pk && (use_buf || (LPL == 64 && DPL == 16))))
+    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_pk && (use_buf || LPL == 64)))
         return hipErrorInvalidValue;
-    if (total > 0)
-        hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
+    if (total <= 0) return hipSuccess;
+    if constexpr (LPL == 64 && DPL == 8 && !SAT && sizeof(VT) == 2) {
+        if (!use_buf && use_pk) {     // volumes past 4 GB: the rebased packed form (k_ocv_paths REBK)
+            hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT, true>), dim3(total), dim3(64), 0, st, C, vols, vol_elems,
+                               trash_off, g, dirmask, a, b, use_buf, use_pk, ilv);
+            return hipSuccess;
+        }
+    }
+    hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT>), dim3(total), dim3(64), 0, st, C, vols, vol_elems, trash_off, g,
                        dirmask, a, b, use_buf, use_pk, ilv);
     return hipSuccess;
 }
@@ -2602,8 +2612,8 @@ int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
     const int pmask = skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask;
     const int dpl = ocv_paths_dpl(g, pmask);
     if (dpl != 8 && dpl != 16) return 0;
-    // 32-bit buffer offsets, or 64-lane lines of 16 values (rebased per step, any volume size)
-    const bool reb = ocv_lanes_per_line(g, pmask) == 64 && dpl == 16;
+    // 32-bit buffer offsets, or 64-lane lines (rebased per step, any volume size)
+    const bool reb = ocv_lanes_per_line(g, pmask) == 64;
     if (!reb && ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF"))) return 0;
     // D > 512: only the fused vertical WTA reads deficits (the row WTA k_ocv_wta64 reads int16 L)
     if (g.D > 512 && skipdir < 0) return 0;

@@ -81,11 +81,13 @@ def test_evol_1080p_both_layouts(engine, synth, pkg, monkeypatch, mode):
     assert np.array_equal(outs["2"], outs["0"]), f"planes: {(outs['2'] != outs['0']).sum()} pixels differ"
 
 
-# 64-lane lines of 16 values (512 < D <= 1024). With SGM_OCV_NO_BUF=1 the packed step rebases its
+# 64-lane lines of 16 values (512 < D <= 1024) and of 8 (256 < D <= 512, their own kernel instantiation).
+# With SGM_OCV_NO_BUF=1 the packed step rebases its
 # buffer descriptors on each step's cell — the form every frame whose volumes pass 4 GB takes (the
 # processing launch's D = 752 at 2448 x 2048: 5.2 GB) — and, under the fused vertical WTA, stores
 # deficit records (vwta 0: the row WTA k_ocv_wta64 reads int16 L, so no deficits there).
-REB_GEOMS = [(26, 900, 0, 752, 21), (22, 800, 7, 640, 9), (20, 1150, -3, 1024, 5), (24, 700, 0, 528, 15)]
+REB_GEOMS = [(26, 900, 0, 752, 21), (22, 800, 7, 640, 9), (20, 1150, -3, 1024, 5), (24, 700, 0, 528, 15),
+             (28, 700, 20, 320, 11), (26, 760, 0, 512, 21)]     # 8 values per lane: the REBK kernel
 
 
 @pytest.mark.parametrize("nobuf", ["0", "1"], ids=["offsets", "rebased"])

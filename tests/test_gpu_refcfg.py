@@ -175,3 +175,19 @@ def test_processing_config_full_frame_vs_oracle(engine, oracle, pkg, proc_frame,
     monkeypatch.setenv("SGM_OCV_GATE", "0")
     got32 = engine.match(left, right)
     assert np.array_equal(got32, ref), f"int32 volumes: {(got32 != ref).sum()} pixels differ"
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", ["sgbm", "hh"])
+def test_capture_size_d512_full_frame_vs_oracle(engine, oracle, pkg, synth, mode):
+    """The capture size with D = 512 from minD 0 (the launch values with a range just past the shipped
+    480): 4.06 GB int16 volumes, the largest a 64-lane line of 8 values meets at this size and just
+    below the 32-bit buffer range (4.29 GB: the buffer offsets run to within 6 % of their wrap),
+    deficit records through the fused vertical WTA; bit for bit against the oracle."""
+    left, right, _ = synth.stereo_pair(REF_H, REF_W, 0, 512, seed=512)
+    p = pkg.default_params(pkg.MODE_OCV_SGBM5 if mode == "sgbm" else pkg.MODE_OCV_HH8, **dict(PROC_KW, num_disparities=512))
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+    assert (ref != -16).mean() > 0.5

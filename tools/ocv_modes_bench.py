@@ -60,6 +60,10 @@ def main():
     for mname, mode in (("MODE_SGBM", pkg.MODE_OCV_SGBM5), ("MODE_HH", pkg.MODE_OCV_HH8)):
         cases.append((f"proccfg 2448x2048 minD 0 D 752 block 21 {mname}", 2048, 2448, mode,
                       dict(ref_kw, min_disparity=0, num_disparities=752)))
+    # 12 MP at D = 480: 10.4 GB int16 volumes, 64-lane lines of 8 values past the 32-bit buffer range
+    # (the rebased packed path kernel, REBK)
+    cases.append(("12MP 4096x3000 D=480 MODE_SGBM block 5", 3000, 4096, pkg.MODE_OCV_SGBM5,
+                  dict(num_disparities=480, min_disparity=0, block_size=5, speckle_window_size=0)))
     eng = pkg.Engine(0)
     st = torch.cuda.Stream()
     for name, h, w, mode, kw in cases:
