@@ -191,3 +191,17 @@ def test_capture_size_d512_full_frame_vs_oracle(engine, oracle, pkg, synth, mode
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
     assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
     assert (ref != -16).mean() > 0.5
+
+
+@pytest.mark.timeout(1100)
+def test_12mp_d480_rebased_full_frame_vs_oracle(engine, oracle, pkg, synth):
+    """A 4096 x 3000 D=480 MODE_SGBM frame: 10.4 GB int16 volumes, so 64-lane lines of 8 values run
+    the step-rebased packed kernel (REBK) with deficit records and the fused vertical WTA reads them;
+    bit for bit against the oracle (the single-threaded restatement takes about a minute on the box)."""
+    left, right, _ = synth.stereo_pair(3000, 4096, 0, 480, seed=4096, with_truth=False)
+    p = pkg.default_params(pkg.MODE_OCV_SGBM5, min_disparity=0, num_disparities=480, block_size=5,
+                           speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
