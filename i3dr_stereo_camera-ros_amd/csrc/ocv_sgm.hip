@@ -30,7 +30,8 @@ constexpr int kMaxCost = 32767;
 #define SGM_OCV_PF 8       // cost rows in flight per path line (D <= 64)
 #endif
 #ifndef SGM_OCV_PRIO
-#define SGM_OCV_PRIO 0     // longest-remaining-first wave priority (lr_prio) in k_ocv_paths
+#define SGM_OCV_PRIO 1     // longest-remaining-first wave priority (lr_prio) in k_ocv_paths: 1 on the packed
+                           // lines of <= 4 dwords per lane, 2 on every line, 0 off
 #endif
 #ifndef SGM_OCV_VWTA_THR
 #define SGM_OCV_VWTA_THR 0   // k_ocv_vwta: uniqueness as one threshold per pixel (A/B knob)
@@ -1575,8 +1576,16 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                         st_b += bstep;
                     }
                 };
+                // longest-remaining-first priority (lr_prio) on lines of <= 4 dwords per lane: the
+                // lines that still have the most steps are served first when the frame's waves
+                // compete (interleaved A/B, frame ms off -> on: C1 0.199 -> 0.190, 1080p D=128
+                // MODE_SGBM 1.389 -> 1.357, MODE_HH 1.937 -> 1.914, 12 MP D=128 MODE_SGBM 8.54 ->
+                // 8.31, the shipped D=480 MODE_SGBM 10.31 -> 10.23, MODE_HH 15.59 -> 15.38, 12 MP
+                // D=480 25.46 -> 25.22; 8 dwords (D=752 MODE_HH 21.75 -> 21.80) and the int branches
+                // (int32 volumes MODE_HH 19.95 -> 20.07) keep it off; profiles/r06_ocv_prio_ab.jsonl)
+                constexpr bool kPrio = SGM_OCV_PRIO == 2 || (SGM_OCV_PRIO == 1 && M <= 4);
                 for (int i0 = 0; i0 < nmax; i0 += PF) {
-                    if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+                    if (kPrio && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
                     steps(i0);
                 }
             };
@@ -1641,7 +1650,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         };
         if (nmax > 0) steps(0, std::true_type{});
         for (int i0 = PF; i0 < nmax; i0 += PF) {
-            if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+            if (SGM_OCV_PRIO == 2 && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
             steps(i0, std::false_type{});
         }
     } else {
@@ -1679,7 +1688,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         };
         if (nmax > 0) steps(0, std::true_type{});
         for (int i0 = PF; i0 < nmax; i0 += PF) {
-            if (SGM_OCV_PRIO && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
+            if (SGM_OCV_PRIO == 2 && (i0 & 15) < PF) lr_prio(nmax - i0, max(g.width1, g.H));
             steps(i0, std::false_type{});
         }
     }
