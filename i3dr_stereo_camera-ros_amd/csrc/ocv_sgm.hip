@@ -567,6 +567,11 @@ template <int R, int DPC, int I, int TRK>
 #ifndef SGM_FUSE_DPC16_PART
 #define SGM_FUSE_DPC16_PART 1    // 16 pairs per block row (a partial last chunk) for D % 32 == 16, D >= 256
 #endif
+#ifndef SGM_FUSE_LDS_PIPE
+#define SGM_FUSE_LDS_PIPE 1      // a pair's right entries read from LDS one pair ahead: 1 for boxes wider than
+#endif                           // 9 (already at 128 VGPRs: shipped block 21 cost 1.856 -> 1.838 ms), 2 always
+                                 // (1080p block 5: 128 -> 155 VGPRs, one block per CU, 0.206 -> 0.256 ms;
+                                 // profiles/r06_ocv_cost_pipe_ab.jsonl), 0 never
 #ifndef SGM_FUSE_WPE
 #define SGM_FUSE_WPE -1          // waves per SIMD asked of the compiler (4: <= 128 VGPRs); -1: 4 for R > 9
 #endif
@@ -733,17 +738,37 @@ void k_ocv_cost_fused(const uint32_t* __restrict__ bt, Geom g, int fullDP,
             for (int c = 0; c < 2; c++) { u[c] = wd(Lk, 3 * c); ulo[c] = wd(Lk, 3 * c + 1); uhi[c] = wd(Lk, 3 * c + 2); }
             const uint32_t* Rk = S + rk_off;
             uint32_t P[I];
+            // kPipe (SGM_FUSE_LDS_PIPE): the right entries of pair q + 1 read from LDS before pair
+            // q's arithmetic (else hipcc issues each pair's reads just before their use)
+            constexpr bool kPipe = SGM_FUSE_LDS_PIPE == 2 || (SGM_FUSE_LDS_PIPE == 1 && R > 9);
+            u16x2_t rw[2][6];
+            auto rload = [&](int q, u16x2_t (&r)[6]) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) r[k] = wd(Rk, 7 * q + k);
+            };
+            if constexpr (kPipe) {
+                rload(0, rw[0]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int q = 0; q < I; q++) {
+                if constexpr (kPipe) {
+                    if (q + 1 < I) rload(q + 1, rw[(q + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    rload(q, rw[q & 1]);
+                }
+                const u16x2_t (&r)[6] = rw[q & 1];
                 u16x2_t m[2];
 #pragma unroll
                 for (int c = 0; c < 2; c++) {
-                    const u16x2_t vv = wd(Rk, 7 * q + 3 * c), v0 = wd(Rk, 7 * q + 3 * c + 1), v1 = wd(Rk, 7 * q + 3 * c + 2);
+                    const u16x2_t vv = r[3 * c], v0 = r[3 * c + 1], v1 = r[3 * c + 2];
                     const u16x2_t c0 = __builtin_elementwise_max(sat(u[c], v1), sat(v0, u[c]));
                     const u16x2_t c1 = __builtin_elementwise_max(sat(vv, uhi[c]), sat(ulo[c], vv));
                     m[c] = __builtin_elementwise_min(c0, c1);
                 }
                 P[q] = __builtin_bit_cast(uint32_t, m[0] + (m[1] >> (u16x2_t){2, 2}));
+                if constexpr (kPipe) __builtin_amdgcn_sched_barrier(0);
             }
             auto upd = [&](auto ss) {
                 constexpr int s2 = decltype(ss)::value;
