@@ -2602,7 +2602,8 @@ constexpr int kOcvWideLineWaves = 1536;     // 16-lane waves below which 32 lane
 #define SGM_OCV_LPL_MID 64                  // lanes per line for 256 < D <= 512 (32 or 64: the shipped D=480
                                             // MODE_SGBM paths 5.96 -> 5.63 ms, MODE_HH 11.2 -> 10.0, profiles/r05_ocv_lpl64_ab.jsonl)
 #endif
-static int ocv_lanes_per_line(const Geom& g, int dirmask)
+// fused_v: the frame's vertical direction runs in the fused vertical WTA (skipdir >= 0)
+static int ocv_lanes_per_line(const Geom& g, int dirmask, bool fused_v)
 {
     if (g.D <= 32) return 16;
     if (g.D > 512) return 64;       // a line per wave: 16 or 32 values per lane (D <= 2048)
@@ -2612,6 +2613,13 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
                                     // of 8 values beat 32 of 16 once the packed step keeps 16 rows
                                     // in flight (5.63 vs 5.96 ms)
     if (const char* e = getenv("SGM_OCV_LPL")) return atoi(e) == 32 ? 32 : 16;
+    // 128 < D <= 256 beside the fused vertical WTA (int16 L volumes either way): 32 lanes of 8
+    // values, the packed step's 4-dword shape (16 rows in flight, the wave priority), instead of
+    // 16 lanes of 16 (interleaved A/B, frame ms: 1080p D=256 MODE_HH 5.51 -> 4.48, 12 MP D=256
+    // MODE_HH 29.4 -> 27.0, MODE_SGBM 19.53 -> 18.86); with the row WTA the 16-lane lines write
+    // deficit records at 16 values per lane and stay ahead (1080p D=256 MODE_SGBM 2.44 vs 2.51;
+    // profiles/r06_ocv_lpl32_d256_ab.jsonl)
+    if (fused_v && g.D > 128) return 32;
     int waves = 0;
     for (int i = 0; i < 8; i++)
         if ((dirmask >> i) & 1)
@@ -2620,9 +2628,9 @@ static int ocv_lanes_per_line(const Geom& g, int dirmask)
 }
 
 // the values per lane launch_ocv_paths picks for the frame
-static int ocv_paths_dpl(const Geom& g, int dirmask)
+static int ocv_paths_dpl(const Geom& g, int dirmask, bool fused_v)
 {
-    const int D = g.D, lpl = ocv_lanes_per_line(g, dirmask);
+    const int D = g.D, lpl = ocv_lanes_per_line(g, dirmask, fused_v);
     if (lpl == 64) return D <= 512 ? 8 : D <= 1024 ? 16 : 32;
     if (lpl == 32) return D <= 64 ? 2 : D <= 128 ? 4 : D <= 256 ? 8 : 16;
     return dpl_for(D);
@@ -2644,10 +2652,10 @@ int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
     if (e && std::atoi(e) == 0) return 0;
     if (g.wide == 1 || g.P2 > 511 || g.P1 > 32768 || g.D > 1024 || g.width1 <= 0) return 0;
     const int pmask = skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask;
-    const int dpl = ocv_paths_dpl(g, pmask);
+    const int dpl = ocv_paths_dpl(g, pmask, skipdir >= 0);
     if (dpl != 8 && dpl != 16) return 0;
     // 32-bit buffer offsets, or 64-lane lines (rebased per step, any volume size)
-    const bool reb = ocv_lanes_per_line(g, pmask) == 64;
+    const bool reb = ocv_lanes_per_line(g, pmask, skipdir >= 0) == 64;
     if (!reb && ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF"))) return 0;
     // D > 512: only the fused vertical WTA reads deficits (the row WTA k_ocv_wta64 reads int16 L)
     if (g.D > 512 && skipdir < 0) return 0;
@@ -2663,7 +2671,7 @@ hipError_t launch_ocv_paths(const int16_t* C, const int16_t* Csat, void* vols, s
 {
     const int D = g.D;
     hipError_t e = hipSuccess;
-    const int lpl = ocv_lanes_per_line(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask);
+    const int lpl = ocv_lanes_per_line(g, skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask, skipdir >= 0);
     if (lpl == 64) {
         if (D <= 512) e = launch_ocv_paths_v<8, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);
         else if (D <= 1024) e = launch_ocv_paths_v<16, 64>(C, Csat, vols, cells, g, dirmask, st, skipdir);

@@ -49,6 +49,13 @@ def main():
          dict(num_disparities=128, min_disparity=0, block_size=5, speckle_window_size=0)),
         ("12MP 4096x3000 D=256 MODE_HH block 5", 3000, 4096, pkg.MODE_OCV_HH8,
          dict(num_disparities=256, min_disparity=0, block_size=5, speckle_window_size=0)),
+        # 128 < D <= 256 in the other shapes (the path lines' width for that range, ocv_lanes_per_line)
+        ("12MP 4096x3000 D=256 MODE_SGBM block 5", 3000, 4096, pkg.MODE_OCV_SGBM5,
+         dict(num_disparities=256, min_disparity=0, block_size=5, speckle_window_size=0)),
+        ("1920x1080 D=256 MODE_SGBM block 5", 1080, 1920, pkg.MODE_OCV_SGBM5,
+         dict(num_disparities=256, min_disparity=0, block_size=5, speckle_window_size=0)),
+        ("1920x1080 D=256 MODE_HH block 5", 1080, 1920, pkg.MODE_OCV_HH8,
+         dict(num_disparities=256, min_disparity=0, block_size=5, speckle_window_size=0)),
     ]
     ref_kw = dict(min_disparity=147, num_disparities=480, block_size=21, uniqueness_ratio=2, speckle_window_size=1000,
                   speckle_range=4, prefilter_cap=7, p1=200, p2=400)
