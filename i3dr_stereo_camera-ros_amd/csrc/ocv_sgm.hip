@@ -2645,6 +2645,11 @@ static int ocv_paths_dpl(const Geom& g, int dirmask, bool fused_v)
 #ifndef SGM_OCV_EVOL
 #define SGM_OCV_EVOL 1
 #endif
+#ifndef SGM_OCV_EVOL_VW_MIND
+#define SGM_OCV_EVOL_VW_MIND 128   // beside the fused vertical WTA, deficits only for D above this: at
+#endif                             // 128 < D <= 256 the 32-lane path lines of 8 values write them (1080p D=256
+                                   // MODE_HH paths 2.45 -> 2.11 ms, frame 4.49 -> 4.25; the fused kernel reads
+                                   // them in the same time; profiles/r06_ocv_evol_d256_ab.jsonl)
 int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
 {
     if (SGM_OCV_EVOL == 0 || SGM_OCV_PK == 0) return 0;
@@ -2659,9 +2664,9 @@ int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
     if (!reb && ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF"))) return 0;
     // D > 512: only the fused vertical WTA reads deficits (the row WTA k_ocv_wta64 reads int16 L)
     if (g.D > 512 && skipdir < 0) return 0;
-    // the fused vertical WTA reads them from 8 values per lane (D > 256): with 2 or 4 the byte and
+    // the fused vertical WTA reads them from 4 or more values per lane (D > 128): with 2 the byte and
     // bit loads per direction cost more than they save (1080p D=128 MODE_HH 2.48 -> 2.95 ms)
-    if (skipdir >= 0 && g.D <= 256) return 0;
+    if (skipdir >= 0 && g.D <= SGM_OCV_EVOL_VW_MIND) return 0;
     if (e && (std::atoi(e) == 1 || std::atoi(e) == 2)) return std::atoi(e);
     return g.D % 128 == 0 ? 2 : 1;
 }
