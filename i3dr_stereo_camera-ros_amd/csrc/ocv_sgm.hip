@@ -1292,6 +1292,12 @@ __device__ __forceinline__ int line_min_i32(int v)
 constexpr uint32_t kBufDrop = 0xFFFFFF00u;
 
 // a 64-bit value the caller knows to be wave-uniform, stated so (kept in SGPRs)
+__device__ __forceinline__ long long lane64(long long v, int lane)   // lane `lane`'s v, wave-uniform
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)v >> 32), lane);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
 __device__ __forceinline__ long long uni64(long long v)
 {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -1514,8 +1520,10 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
         // 512 on frames past 4 GiB of volume, e.g. 12 MP) in their own instantiation (REBK), because
         // the per-step descriptors of 16 rows in flight cost SGPRs that the buffer-offset form of the
         // same kernel (the shipped D=480 config) would otherwise pay for (105 -> 138 VGPRs); 32 values
-        // (D > 1024) have a lane straddling D that would load past its rebased cell.
-        if (use_pk && (use_buf || (LPL == 64 && (DPL == 16 || REBK)))) {
+        // (D > 1024) have a lane straddling D that would load past its rebased cell. 32-lane lines of
+        // 8 values (128 < D <= 256 beside the fused vertical WTA, 12 MP frames past 4 GiB) take the
+        // same REBK instantiation with one descriptor per half-wave line.
+        if (use_pk && (use_buf || (LPL == 64 && (DPL == 16 || REBK)) || (LPL == 32 && REBK))) {
             constexpr int M = DPL / 2;
             const size_t cells = (size_t)g.width1 * g.H * g.D;
             const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(uint32_t)(cells * 2), 0x00020000);
@@ -1547,14 +1555,43 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
             uint32_t ev_lo = (uint32_t)(pix0 * el.ls + dl), ev_hi = (uint32_t)(el.hb + pix0 * el.hs + dl / 8);
             const uint32_t ev_step = (uint32_t)(pstep * el.ls), ev_hstep = (uint32_t)(pstep * el.hs);
             // rebased form (REB): the line's cell / pixel of step i (clamped to its last step, so every
-            // descriptor base stays inside the volume), stated wave-uniform
-            const long long ucb = uni64(cbase), ucs = uni64(cstep), upx = uni64(pix0), ups = uni64(pstep);
-            const int ulast = __builtin_amdgcn_readfirstlane(ilast);
+            // descriptor base stays inside the volume), stated uniform over the line: the wave's one
+            // line (64 lanes), or the two half-wave lines' (32 lanes): one descriptor then spans both
+            // lines' cells of the step (adjacent lines of one direction, lengths within a step of each
+            // other: a few rows apart at most) and each lane adds its own line's distance from the lower
+            constexpr int NH = LPL == 32 ? 2 : 1;
+            long long ucb[NH], ucs[NH], upx[NH], ups[NH];
+            int ulast[NH];
+#pragma unroll
+            for (int h = 0; h < NH; h++) {
+                ucb[h] = NH == 1 ? uni64(cbase) : lane64(cbase, 32 * h);
+                ucs[h] = NH == 1 ? uni64(cstep) : lane64(cstep, 32 * h);
+                upx[h] = NH == 1 ? uni64(pix0) : lane64(pix0, 32 * h);
+                ups[h] = NH == 1 ? uni64(pstep) : lane64(pstep, 32 * h);
+                ulast[h] = NH == 1 ? __builtin_amdgcn_readfirstlane(ilast) : __builtin_amdgcn_readlane(ilast, 32 * h);
+            }
+            if constexpr (NH == 2) {
+                // a second half past the direction's last line (n = 0) follows the first one's line
+                if (!__builtin_amdgcn_readlane((int)(line < nlines), 32)) {
+                    ucb[1] = ucb[0]; ucs[1] = ucs[0]; upx[1] = upx[0]; ups[1] = ups[0]; ulast[1] = ulast[0];
+                }
+            }
             const uint32_t cell_bytes = (uint32_t)g.D * 2u;
-            auto rs_cell = [&](const void* base, int i) {
-                return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (ucb + (long long)min(i, ulast) * ucs) * 2),
-                                                         0, (int)cell_bytes, 0x00020000);
+            // elements a, b (the two half-lines' cells or pixels of a step, `unit` bytes apart) under one
+            // descriptor from the lower one to `extra` bytes past the higher; off: the lane's own offset
+            auto span = [&](const void* base, long long a, long long b, long long unit, uint32_t extra, uint32_t& off) {
+                if constexpr (NH == 1) {                 // one line per wave: the element's own descriptor
+                    off = 0;
+                    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + a * unit), 0, (int)extra, 0x00020000);
+                } else {
+                    const long long lo = a < b ? a : b, d = a < b ? b - a : a - b;
+                    off = (uint32_t)(((r ? b : a) - lo) * unit);
+                    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + lo * unit), 0,
+                                                             (int)(uint32_t)(d * unit + extra), 0x00020000);
+                }
             };
+            auto cell_at = [&](int h, int i) { return ucb[h] + (long long)min(i, ulast[h]) * ucs[h]; };
+            auto px_at = [&](int h, int i) { return upx[h] + (long long)min(i, ulast[h]) * ups[h]; };
             auto run = [&](auto evc, auto rebc) {
                 constexpr bool EV = decltype(evc)::value;
                 constexpr bool REB = decltype(rebc)::value;
@@ -1563,8 +1600,14 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                 for (int i = 0; i < M; i++) L2[i] = 0;
                 uint32_t delta2 = P2 * 0x10001u;         // the path's first pixel: L = C - P2
                 auto loadC = [&](int i, uint32_t (&c)[M]) {
-                    if constexpr (REB) bload_dw<M>(rs_cell(C, i), (uint32_t)dl * 2u, c);
-                    else { bload_dw<M>(rsC, ld_b, c); ld_b += bstep; }
+                    if constexpr (REB) {
+                        uint32_t off;
+                        const auto rs = span(C, cell_at(0, i), cell_at(NH - 1, i), 2, cell_bytes, off);
+                        bload_dw<M>(rs, off + (uint32_t)dl * 2u, c);
+                    } else {
+                        bload_dw<M>(rsC, ld_b, c);
+                        ld_b += bstep;
+                    }
                 };
 #pragma unroll
                 for (int q = 0; q < PF; q++) loadC(q, C2[q]);
@@ -1576,18 +1619,22 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                         const uint32_t lmin = ocv_step_pk<DPL, LPL>(C2[q], L2, delta2, P1P1, imask, p, EV ? E2 : nullptr);
                         const bool ok = lane_act && i < n;
                         if constexpr (EV && REB) {
-                            const long long px = upx + (long long)min(i, ulast) * ups;
-                            const auto rlo = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)V + px * el.ls), 0, (int)el.ls, 0x00020000);
-                            const auto rhi = __builtin_amdgcn_make_buffer_rsrc((void*)((char*)V + el.hb + px * el.hs), 0,
-                                                                               (int)el.hs, 0x00020000);
-                            evol_store<DPL>(rlo, ok ? (uint32_t)dl : kBufDrop, rhi, ok ? (uint32_t)dl / 8u : kBufDrop, E2);
+                            const long long pa = px_at(0, i), pb = px_at(NH - 1, i);
+                            uint32_t olo, ohi;
+                            const auto rlo = span(V, pa, pb, el.ls, el.ls, olo);
+                            const auto rhi = span((const char*)V + el.hb, pa, pb, el.hs, el.hs, ohi);
+                            evol_store<DPL>(rlo, ok ? olo + (uint32_t)dl : kBufDrop, rhi, ok ? ohi + (uint32_t)dl / 8u : kBufDrop, E2);
                         } else if constexpr (EV) {
                             evol_store<DPL>(rsV, ok ? ev_lo : kBufDrop, rsV, ok ? ev_hi : kBufDrop, E2);
                             ev_lo += ev_step;
                             ev_hi += ev_hstep;
                         } else {
-                            const auto rsS = REB ? rs_cell(V, i) : rsV;
-                            const uint32_t so = REB ? (uint32_t)dl * 2u : st_b;
+                            uint32_t so = st_b;
+                            auto rsS = rsV;
+                            if constexpr (REB) {
+                                rsS = span(V, cell_at(0, i), cell_at(NH - 1, i), 2, cell_bytes, so);
+                                so += (uint32_t)dl * 2u;
+                            }
                             if constexpr (DPL == 32) {   // two halves: the straddling lane drops its upper one
                                 bstore_dw<8>(rsS, ok ? so : kBufDrop, *reinterpret_cast<const uint32_t(*)[8]>(&L2[0]));
                                 bstore_dw<8>(rsS, ok && !straddle ? so + 32u : kBufDrop,
@@ -1614,7 +1661,7 @@ __global__ __launch_bounds__(64) void k_ocv_paths(const int16_t* __restrict__ C,
                     steps(i0);
                 }
             };
-            if constexpr (LPL == 64 && (DPL == 16 || REBK)) {
+            if constexpr ((LPL == 64 && (DPL == 16 || REBK)) || (LPL == 32 && REBK)) {
                 if (!use_buf) {
                     {
                         if (g.evol) {
@@ -2561,10 +2608,11 @@ static hipError_t launch_ocv_paths_l(const int16_t* C, void* vols_, size_t cells
     // buffer offsets or 64-lane rebased descriptors); ocv_evol_mode decided g.evol from the same conditions, and the WTA reads
     // deficits whenever it is set: refuse a frame where the two disagree rather than hand the WTA
     // int16 L volumes it would read as deficits (flagged kernels ignore evol and write full volumes)
-    if (!SAT && sizeof(VT) == 2 && g.evol && !((DPL == 8 || DPL == 16) && use_pk && (use_buf || LPL == 64)))
+    if (!SAT && sizeof(VT) == 2 && g.evol &&
+        !((DPL == 8 || DPL == 16) && use_pk && (use_buf || LPL == 64 || (LPL == 32 && DPL == 8))))
         return hipErrorInvalidValue;
     if (total <= 0) return hipSuccess;
-    if constexpr (LPL == 64 && DPL == 8 && !SAT && sizeof(VT) == 2) {
+    if constexpr ((LPL == 64 || LPL == 32) && DPL == 8 && !SAT && sizeof(VT) == 2) {
         if (!use_buf && use_pk) {     // volumes past 4 GB: the rebased packed form (k_ocv_paths REBK)
             hipLaunchKernelGGL((k_ocv_paths<DPL, LPL, VT, SAT, true>), dim3(total), dim3(64), 0, st, C, vols, vol_elems,
                                trash_off, g, dirmask, a, b, use_buf, use_pk, ilv);
@@ -2659,8 +2707,9 @@ int ocv_evol_mode(const Geom& g, int dirmask, int skipdir)
     const int pmask = skipdir >= 0 ? dirmask & ~(1 << skipdir) : dirmask;
     const int dpl = ocv_paths_dpl(g, pmask, skipdir >= 0);
     if (dpl != 8 && dpl != 16) return 0;
-    // 32-bit buffer offsets, or 64-lane lines (rebased per step, any volume size)
-    const bool reb = ocv_lanes_per_line(g, pmask, skipdir >= 0) == 64;
+    // 32-bit buffer offsets, or 64-lane lines / 32-lane lines of 8 values (rebased per step, any size)
+    const int lpl = ocv_lanes_per_line(g, pmask, skipdir >= 0);
+    const bool reb = lpl == 64 || (lpl == 32 && dpl == 8);
     if (!reb && ((size_t)g.width1 * g.H * g.D * 2 >= (size_t)kBufDrop || std::getenv("SGM_OCV_NO_BUF"))) return 0;
     // D > 512: only the fused vertical WTA reads deficits (the row WTA k_ocv_wta64 reads int16 L)
     if (g.D > 512 && skipdir < 0) return 0;

@@ -276,11 +276,17 @@ def test_ocv_device_batch_lanes(engine, oracle, synth, pkg, monkeypatch, streams
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("h,w,minD,D,block,compat", [(48, 600, 0, 144, 5, 7), (40, 640, -7, 208, 9, 0),
                                                      (36, 700, 5, 256, 3, 7), (30, 520, 2, 160, 7, 0)])
-def test_ocv_fused_vertical_32_lane_lines(engine, oracle, synth, pkg, monkeypatch, mode, h, w, minD, D, block, compat):
+@pytest.mark.parametrize("nobuf", ["", "1"], ids=["buf32", "rebased"])
+def test_ocv_fused_vertical_32_lane_lines(engine, oracle, synth, pkg, monkeypatch, mode, h, w, minD, D, block, compat,
+                                          nobuf):
     """128 < D <= 256 beside the fused vertical WTA (forced here with SGM_OCV_VWTA=1; large frames
     take it by default): the path lines are 32 lanes of 8 values (ocv_lanes_per_line), the packed
-    4-dword step with the wave priority; bit-exact vs the oracle in both modes and compat builds."""
+    4-dword step with the wave priority, writing deficit records; with SGM_OCV_NO_BUF=1 the
+    rebased form of volumes past 4 GiB (one descriptor per half-wave line, k_ocv_paths REBK);
+    bit-exact vs the oracle in both modes and compat builds."""
     monkeypatch.setenv("SGM_OCV_VWTA", "1")
+    if nobuf:
+        monkeypatch.setenv("SGM_OCV_NO_BUF", nobuf)
     left, right, _ = synth.stereo_pair(h, w, max(minD, 0), D, seed=h * D)
     p = pkg.default_params(mode, min_disparity=minD, num_disparities=D, block_size=block, ocv_compat=compat)
     engine.set_params(p)
@@ -297,6 +303,19 @@ def test_ocv_1080p_d256_full_frame_vs_oracle(engine, oracle, synth, pkg, mode):
     against the oracle."""
     left, right, _ = synth.stereo_pair(1080, 1920, 0, 256, seed=256, with_truth=False)
     p = pkg.default_params(mode, min_disparity=0, num_disparities=256, block_size=5, speckle_window_size=0)
+    engine.set_params(p)
+    got = engine.match(left, right)
+    ref = oracle.match(to_oracle_params(oracle, p), left, right)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} pixels differ"
+
+
+@pytest.mark.timeout(900)
+def test_ocv_12mp_d256_hh_rebased_full_frame_vs_oracle(engine, oracle, synth, pkg):
+    """A 4096 x 3000 D=256 MODE_HH frame: 5.9 GB volumes, so the 32-lane path lines of 8 values run the
+    rebased packed kernel (one descriptor per half-wave line) and write deficit records that the
+    fused vertical WTA reads; bit for bit against the oracle."""
+    left, right, _ = synth.stereo_pair(3000, 4096, 0, 256, seed=4256, with_truth=False)
+    p = pkg.default_params(1, min_disparity=0, num_disparities=256, block_size=5, speckle_window_size=0)
     engine.set_params(p)
     got = engine.match(left, right)
     ref = oracle.match(to_oracle_params(oracle, p), left, right)
