@@ -1314,6 +1314,12 @@ __device__ __forceinline__ long long uni64(long long v)
 #ifndef SGM_OCV_VWTA_PK_EV5
 #define SGM_OCV_VWTA_PK_EV5 1  // k_ocv_vwta_pk also for MODE_SGBM when the volumes are deficit records
 #endif
+#ifndef SGM_OCV_VWTA_PK_MIND
+#define SGM_OCV_VWTA_PK_MIND 4  // k_ocv_vwta_pk from this many values per lane: 4 (128 < D <= 256, deficit
+                                // records in half groups) against the int kernel, frame ms: 12 MP D=256 MODE_HH
+                                // 25.4 -> 23.95, MODE_SGBM 17.48 -> 16.18, 1080p D=256 MODE_HH 4.22 -> 4.17
+                                // (profiles/r06_ocv_vwta_pk4_ab.jsonl)
+#endif
 #ifndef SGM_OCV_VWTA_PK_PF
 #define SGM_OCV_VWTA_PK_PF 0  // k_ocv_vwta_pk steps in flight (0: by shape)
 #endif
@@ -2851,10 +2857,20 @@ __device__ __forceinline__ int line_sum_i32(int v)
     return v;
 }
 // The packed pairs of the lane's deficits (Geom::evol) from its raw loads: w[0 .. M/2) the byte
-// plane's dwords, w[M/2] the bit-plane bytes (DPL = 8 or 16)
+// plane's dwords, w[M/2] the bit-plane bytes (DPL = 8 or 16; DPL = 4: half a group, hsh = 2 for
+// its upper half, whose bits sit two places up in each nibble)
 template <int M>
-__device__ __forceinline__ void evol_pairs(const uint32_t (&w)[M], uint32_t (&e2)[M])
+__device__ __forceinline__ void evol_pairs(const uint32_t (&w)[M], uint32_t (&e2)[M], int hsh = 0)
 {
+    if constexpr (M == 2) {
+        const uint32_t h2 = (((w[1] & 0xFFu) >> hsh) * 0x1001u) & 0x000F000Fu;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const uint32_t lo2 = __builtin_amdgcn_perm(0u, w[0], i ? 0x0C030C02u : 0x0C010C00u);
+            e2[i] = ((h2 << (8 - i)) & 0x01000100u) | lo2;
+        }
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < M / 4; c++) {
         // evens of the group at bits 0-3, odds at bits 16-19
@@ -2896,7 +2912,7 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
         const int y = F == 0 ? min(i, g.H - 1) : max(g.H - 1 - i, 0);
         return ((size_t)y * g.width1 + x1) * g.D + dl;
     };
-    static_assert(!EV || DPL == 8 || DPL == 16, "deficit planes: 8 or 16 values per lane");
+    static_assert(!EV || DPL == 4 || DPL == 8 || DPL == 16, "deficit planes: 4, 8 or 16 values per lane");
     auto load = [&](int i, uint32_t (&c)[M], uint32_t (&v)[NDIR][M]) {
         const size_t o = cell(i);
         load_dw<M>(C + o, c);
@@ -2909,7 +2925,10 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
                 const uint8_t* vb = (const uint8_t*)(vols + (size_t)s * vol_elems);
                 const uint8_t* lo = vb + px * el.ls + dl;
                 const uint8_t* hi = vb + el.hb + px * el.hs + dl / 8;
-                if constexpr (DPL == 8) {
+                if constexpr (DPL == 4) {
+                    v[s][0] = *(const uint32_t*)lo;
+                    v[s][1] = *hi;
+                } else if constexpr (DPL == 8) {
                     const uint2 t = *(const uint2*)lo;
                     v[s][0] = t.x; v[s][1] = t.y;
                     v[s][2] = *hi;
@@ -2949,7 +2968,7 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
             if (s == F) continue;
             if constexpr (EV) {
                 uint32_t e2[M];
-                evol_pairs<M>(V[s], e2);
+                evol_pairs<M>(V[s], e2, (dl & 4) >> 1);
 #pragma unroll
                 for (int j = 0; j < M; j++) Lv[s][j] = pk_sub(Cc[j], e2[j]);
             } else {
@@ -3035,7 +3054,7 @@ static void launch_ocv_vwta_l(const int16_t* C, const void* vols, size_t cells, 
     // and 1080p MODE_HH (0.87 vs 0.90-0.94) keep k_ocv_vwta (profiles/r05_ocv_vwta_pk_ab.jsonl):
     // the kernel streams its volumes near the read peak, and fewer instructions help only where
     // the operands of more steps fit in flight
-    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= 8) {
+    if constexpr (!SAT && sizeof(VT) == 2 && DPL >= SGM_OCV_VWTA_PK_MIND) {
         if (use_pk && g.uniq < 100 && SGM_OCV_VWTA_PK != 0 && (NDIR == 8 || (g.evol && SGM_OCV_VWTA_PK_EV5))) {
             if constexpr (DPL <= 16) {
                 if (g.evol) {
