@@ -2898,7 +2898,11 @@ __global__ __launch_bounds__(64) void k_ocv_vwta_pk(const int16_t* __restrict__ 
     // against 4.52-4.54 at 2; profiles/r06_ocv_d752_vwta_pf_ab.jsonl). 8 values per lane: MODE_HH over
     // deficit records 4 (the shipped D=480 frame's kernel 4.77 -> 3.68 ms), else 8 (MODE_SGBM 2.95
     // against 3.04 at 4, 2.99 at 6; profiles/r06_ocv_cost_ring0_vwta_pf_ab.jsonl)
+    // 4 values per lane (128 < D <= 256): 6 steps (frame ms of the fused kernel at 2 / 4 / 6 / 8 / 12: 12 MP
+    // D=256 MODE_SGBM 5.81 / 5.22 / 5.22 / 5.62 / 6.03, MODE_HH 6.71 / 7.07 / 7.21 / - / 10.48, 1080p D=256
+    // MODE_HH 1.55-1.72 / 1.57-1.70 / 1.35 / - / 1.89; profiles/r06_ocv_vwta_pk4_pf_ab.jsonl)
     constexpr int PF = SGM_OCV_VWTA_PK_PF > 0 ? SGM_OCV_VWTA_PK_PF
+                       : DPL == 4                 ? 6
                        : DPL >= 32                ? 1
                        : DPL >= 16                ? (NDIR == 5 ? 4 : 2)
                        : (NDIR == 8 && EV)        ? 4
